@@ -1,0 +1,108 @@
+"""ctypes binding of libcsg.so (include/csg_api.h).
+
+The product path has no CPU fallback: if the HIP library is missing or fails
+to load, every call raises :class:`CsgError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libcsg.so")
+
+EXPORTED = (
+    "csg_create", "csg_destroy", "csg_last_error", "csg_abi_version", "csg_upload_scene",
+    "csg_upload_texture", "csg_set_light", "csg_set_instance_transforms", "csg_set_keypoints",
+    "csg_render_batch", "csg_render_batch_async", "csg_synchronize", "csg_get_batch_stats",
+    "csg_project_keypoints",
+)
+
+
+class CsgError(RuntimeError):
+    pass
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("max_frames", C.c_uint32), ("near_clip", C.c_float), ("far_clip", C.c_float),
+                ("records_per_frame", C.c_uint32), ("bins_per_frame", C.c_uint32)]
+
+
+class Mesh(C.Structure):
+    _fields_ = [("positions", C.c_void_p), ("n_vertices", C.c_uint32), ("indices", C.c_void_p),
+                ("n_tris", C.c_uint32), ("uvs", C.c_void_p), ("n_uvs", C.c_uint32),
+                ("uv_indices", C.c_void_p), ("material", C.c_uint32)]
+
+
+class Material(C.Structure):
+    _fields_ = [("base_color", C.c_uint8 * 4), ("texture", C.c_int32), ("alpha_test", C.c_uint32),
+                ("alpha_threshold", C.c_uint32)]
+
+
+class Instance(C.Structure):
+    _fields_ = [("model", C.c_float * 16), ("mesh", C.c_uint32), ("inst_idx", C.c_int32),
+                ("reserved", C.c_uint32 * 2)]
+
+
+class Light(C.Structure):
+    _fields_ = [("ambient", C.c_float * 3), ("sun", C.c_float * 3), ("sun_dir", C.c_float * 3),
+                ("sky", C.c_uint8 * 4)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("view", C.c_float * 16), ("proj", C.c_float * 16), ("xform_set", C.c_uint32),
+                ("frame_id", C.c_uint32)]
+
+
+class Outputs(C.Structure):
+    _fields_ = [("rgb", C.c_void_p), ("instance", C.c_void_p), ("depth", C.c_void_p),
+                ("keypoints_uv", C.c_void_p), ("keypoints_vis", C.c_void_p), ("inst_stats", C.c_void_p),
+                ("n_labels", C.c_uint32), ("on_device", C.c_int32)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("records", C.c_uint64), ("bin_entries", C.c_uint64), ("ms_setup", C.c_float),
+                ("ms_bin", C.c_float), ("ms_raster", C.c_float), ("ms_keypoints", C.c_float),
+                ("ms_total", C.c_float)]
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libcsg.so, building it first when the sources are newer (needs hipcc)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path) or os.environ.get("CSG_AUTOBUILD", "1") == "1":
+        try:
+            from .build import build, needs_build
+            if needs_build():
+                build()
+        except Exception as e:  # pragma: no cover - surfaced below
+            if not os.path.exists(path):
+                raise CsgError(f"libcsg.so missing and could not be built: {e}") from e
+    if not os.path.exists(path):
+        raise CsgError(f"libcsg.so not found at {path}; run python -m constructionsceneposeestimation_amd.build")
+    lib = C.CDLL(path)
+    vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int32
+    lib.csg_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
+    lib.csg_destroy.argtypes = [vp]
+    lib.csg_destroy.restype = None
+    lib.csg_last_error.argtypes = [vp]
+    lib.csg_last_error.restype = C.c_char_p
+    lib.csg_abi_version.argtypes = []
+    lib.csg_upload_scene.argtypes = [vp, C.POINTER(Mesh), u32, C.POINTER(Material), u32, C.POINTER(Instance), u32]
+    lib.csg_upload_texture.argtypes = [vp, u32, vp, u32, u32]
+    lib.csg_set_light.argtypes = [vp, C.POINTER(Light)]
+    lib.csg_set_instance_transforms.argtypes = [vp, u32, vp, u32]
+    lib.csg_set_keypoints.argtypes = [vp, u32, vp, u32]
+    lib.csg_render_batch.argtypes = [vp, vp, u32, C.POINTER(Outputs)]
+    lib.csg_render_batch_async.argtypes = [vp, vp, u32, i32, C.POINTER(Outputs), vp]
+    lib.csg_synchronize.argtypes = [vp]
+    lib.csg_get_batch_stats.argtypes = [vp, C.POINTER(BatchStats)]
+    lib.csg_project_keypoints.argtypes = [vp, vp, u32, vp, vp, vp, vp]
+    _lib = lib
+    return lib

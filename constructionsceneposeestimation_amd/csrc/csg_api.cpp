@@ -1,0 +1,604 @@
+// C-ABI host side of libcsg.so (see include/csg_api.h).
+//
+// Owns the device copy of the scene (one HBM-resident scene per context,
+// shared by every frame of every batch), the per-batch work buffers sized
+// for `max_frames`, and the launch sequence of csg_kernels.hip.  All
+// validation that protects the GPU from out-of-bounds indices happens here,
+// on the host, before anything is uploaded.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/csg_api.h"
+#include "csg_kernels.h"
+
+using namespace csg;
+
+namespace {
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (count == 0) return hipSuccess;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct HostTexture {
+  std::vector<uint8_t> rgba;
+  uint32_t w = 0, h = 0;
+  bool present = false;
+};
+
+}  // namespace
+
+struct csg_ctx {
+  csg_config cfg{};
+  std::string err;
+  hipStream_t stream = nullptr;
+  uint32_t tiles_x = 0, tiles_y = 0, n_tiles = 0;
+
+  // scene
+  bool have_scene = false;
+  uint32_t n_inst = 0, n_meshes = 0, n_materials = 0;
+  uint64_t n_tris_total = 0;
+  DevBuf<float> pos, uvs;
+  DevBuf<uint32_t> tris, uv_tris, inst_mesh;
+  DevBuf<int32_t> inst_label;
+  DevBuf<MeshDesc> meshes;
+  DevBuf<MatDesc> mats;
+  std::vector<MatDesc> h_mats;
+  std::vector<MeshDesc> h_meshes;
+  DevBuf<Chunk> chunks;
+  uint32_t n_chunks = 0;
+  std::vector<HostTexture> textures;
+  bool tex_dirty = true;
+  DevBuf<uint8_t> texels;
+  DevBuf<TexDesc> texd;
+  float ambient[3] = {0.26f, 0.29f, 0.34f}, sun[3] = {0.78f, 0.78f, 0.78f}, sun_dir[3] = {0.7071f, 0.f, 0.7071f};
+  uint32_t sky = 191u | (217u << 8) | (255u << 16);
+  std::vector<float> h_models;          // [sets][I][16]
+  std::vector<uint8_t> set_valid;
+  DevBuf<float> models;
+  bool models_dirty = true;
+  uint32_t n_kp = 0;
+  std::vector<float> h_kp;              // [sets][K][3]
+  std::vector<uint8_t> kp_valid;
+  DevBuf<float> kp;
+  bool kp_dirty = true;
+
+  // per-batch work buffers
+  uint32_t rec_cap = 0, bin_cap = 0, work_frames = 0;
+  DevBuf<FrameDev> frames;
+  FrameDev* h_frames = nullptr;         // pinned staging
+  DevBuf<float> clip, pv;
+  DevBuf<Rec> recs;
+  DevBuf<uint32_t> rect, rec_count, tile_count, tile_off, tile_fill, bins, overflow;
+  // internal outputs (host-output mode / scratch)
+  DevBuf<uint8_t> o_rgb;
+  DevBuf<int32_t> o_inst;
+  DevBuf<float> o_depth, o_kp_uv;
+  DevBuf<int32_t> o_kp_vis;
+  DevBuf<uint32_t> o_stats;
+
+  // timing
+  bool timing = true;
+  hipEvent_t ev[6] = {};
+  uint32_t last_F = 0;
+
+  int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+};
+
+#define HIP_TRY(ctx, expr)                                                                           \
+  do {                                                                                               \
+    hipError_t _e = (expr);                                                                          \
+    if (_e != hipSuccess)                                                                            \
+      return (ctx)->fail(_e == hipErrorOutOfMemory ? CSG_ERR_OOM : CSG_ERR_DEVICE, "%s: %s", #expr,  \
+                         hipGetErrorString(_e));                                                     \
+  } while (0)
+
+extern "C" {
+
+int csg_abi_version(void) { return CSG_ABI_VERSION; }
+
+const char* csg_last_error(const csg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int csg_create(const csg_config* cfg, csg_ctx** out) {
+  if (!cfg || !out) return CSG_ERR_INVALID;
+  *out = nullptr;
+  if (cfg->width == 0 || cfg->height == 0 || cfg->width > 8192 || cfg->height > 8192 || cfg->max_frames == 0 ||
+      !(cfg->near_clip > 0.f) || !(cfg->far_clip > cfg->near_clip))
+    return CSG_ERR_INVALID;
+  csg_ctx* c = new csg_ctx();
+  c->cfg = *cfg;
+  c->tiles_x = (cfg->width + kTile - 1) / kTile;
+  c->tiles_y = (cfg->height + kTile - 1) / kTile;
+  c->n_tiles = c->tiles_x * c->tiles_y;
+  hipError_t e = hipSetDevice(cfg->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  for (int k = 0; k < 6 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[k]);
+  if (e != hipSuccess) {
+    c->err = hipGetErrorString(e);
+    csg_destroy(c);
+    return CSG_ERR_DEVICE;
+  }
+  *out = c;
+  return CSG_OK;
+}
+
+void csg_destroy(csg_ctx* c) {
+  if (!c) return;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->pos.release(); c->uvs.release(); c->tris.release(); c->uv_tris.release(); c->inst_mesh.release();
+  c->inst_label.release(); c->meshes.release(); c->mats.release(); c->chunks.release(); c->texels.release();
+  c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
+  c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
+  c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
+  c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
+  if (c->h_frames) (void)hipHostFree(c->h_frames);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, const csg_material* materials,
+                     uint32_t n_materials, const csg_instance* inst, uint32_t n_inst) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!meshes || !materials || !inst || n_meshes == 0 || n_materials == 0 || n_inst == 0)
+    return c->fail(CSG_ERR_INVALID, "upload_scene: empty scene");
+  if (n_inst >= kMaxInstances) return c->fail(CSG_ERR_LIMIT, "upload_scene: %u instances >= %u", n_inst, kMaxInstances);
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  std::vector<float> pos, uvs;
+  std::vector<uint32_t> tris, uvt;
+  std::vector<MeshDesc> md(n_meshes);
+  for (uint32_t m = 0; m < n_meshes; ++m) {
+    const csg_mesh& M = meshes[m];
+    if (M.n_tris >= kMaxTrisPerMesh) return c->fail(CSG_ERR_LIMIT, "mesh %u: %u tris >= 2^20", m, M.n_tris);
+    if (M.material >= n_materials) return c->fail(CSG_ERR_INVALID, "mesh %u: material %u out of range", m, M.material);
+    if ((M.n_vertices && !M.positions) || (M.n_tris && !M.indices))
+      return c->fail(CSG_ERR_INVALID, "mesh %u: null arrays", m);
+    for (uint64_t k = 0; k < 3ull * M.n_tris; ++k)
+      if (M.indices[k] >= M.n_vertices) return c->fail(CSG_ERR_INVALID, "mesh %u: index out of range", m);
+    const bool has_uv = M.uvs && M.uv_indices && M.n_uvs;
+    if (has_uv)
+      for (uint64_t k = 0; k < 3ull * M.n_tris; ++k)
+        if (M.uv_indices[k] >= M.n_uvs) return c->fail(CSG_ERR_INVALID, "mesh %u: uv index out of range", m);
+    md[m] = MeshDesc{(uint32_t)(pos.size() / 3), (uint32_t)(tris.size() / 3), M.n_tris, (uint32_t)(uvs.size() / 2),
+                     has_uv ? 1u : 0u, M.material};
+    pos.insert(pos.end(), M.positions, M.positions + 3ull * M.n_vertices);
+    tris.insert(tris.end(), M.indices, M.indices + 3ull * M.n_tris);
+    if (has_uv) {
+      uvs.insert(uvs.end(), M.uvs, M.uvs + 2ull * M.n_uvs);
+      uvt.insert(uvt.end(), M.uv_indices, M.uv_indices + 3ull * M.n_tris);
+    } else {
+      uvt.insert(uvt.end(), 3ull * M.n_tris, 0u);
+    }
+  }
+  if (uvs.empty()) uvs.assign(2, 0.f);
+  std::vector<MatDesc> mats(n_materials);
+  for (uint32_t k = 0; k < n_materials; ++k) {
+    memcpy(mats[k].base, materials[k].base_color, 4);
+    mats[k].texture = materials[k].texture;
+    mats[k].alpha_test = materials[k].alpha_test;
+    mats[k].alpha_threshold = materials[k].alpha_threshold;
+  }
+  std::vector<uint32_t> imesh(n_inst), chunk_inst;
+  std::vector<int32_t> ilabel(n_inst);
+  std::vector<Chunk> ch;
+  std::vector<float> models((size_t)n_inst * 16);
+  uint64_t ntot = 0;
+  for (uint32_t i = 0; i < n_inst; ++i) {
+    if (inst[i].mesh >= n_meshes) return c->fail(CSG_ERR_INVALID, "instance %u: mesh out of range", i);
+    imesh[i] = inst[i].mesh;
+    ilabel[i] = inst[i].inst_idx;
+    memcpy(&models[(size_t)i * 16], inst[i].model, 16 * sizeof(float));
+    const uint32_t nt = md[inst[i].mesh].ntris;
+    for (uint32_t s0 = 0; s0 < nt; s0 += kBlock) ch.push_back(Chunk{i, s0, std::min<uint32_t>(kBlock, nt - s0), 0});
+    ntot += nt;
+  }
+  if (ch.empty()) return c->fail(CSG_ERR_INVALID, "upload_scene: no triangles");
+  HIP_TRY(c, c->pos.alloc(pos.size()));
+  HIP_TRY(c, c->uvs.alloc(uvs.size()));
+  HIP_TRY(c, c->tris.alloc(tris.size()));
+  HIP_TRY(c, c->uv_tris.alloc(uvt.size()));
+  HIP_TRY(c, c->meshes.alloc(n_meshes));
+  HIP_TRY(c, c->mats.alloc(n_materials));
+  HIP_TRY(c, c->inst_mesh.alloc(n_inst));
+  HIP_TRY(c, c->inst_label.alloc(n_inst));
+  HIP_TRY(c, c->chunks.alloc(ch.size()));
+  HIP_TRY(c, hipMemcpy(c->pos.p, pos.data(), pos.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->uvs.p, uvs.data(), uvs.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->tris.p, tris.data(), tris.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->uv_tris.p, uvt.data(), uvt.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->meshes.p, md.data(), md.size() * sizeof(MeshDesc), hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->mats.p, mats.data(), mats.size() * sizeof(MatDesc), hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->inst_mesh.p, imesh.data(), imesh.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->inst_label.p, ilabel.data(), ilabel.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->chunks.p, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice));
+  c->n_inst = n_inst;
+  c->n_meshes = n_meshes;
+  c->n_materials = n_materials;
+  c->h_mats = mats;
+  c->h_meshes = md;
+  c->n_chunks = (uint32_t)ch.size();
+  c->n_tris_total = ntot;
+  c->h_models = models;
+  c->set_valid.assign(1, 1);
+  c->models_dirty = true;
+  c->h_kp.clear();
+  c->kp_valid.clear();
+  c->n_kp = 0;
+  c->kp_dirty = true;
+  c->have_scene = true;
+  c->work_frames = 0;  // re-size work buffers
+  return CSG_OK;
+}
+
+int csg_upload_texture(csg_ctx* c, uint32_t tex_id, const uint8_t* rgba8, uint32_t w, uint32_t h) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!rgba8 || w == 0 || h == 0 || w > 16384 || h > 16384 || tex_id >= 4096)
+    return c->fail(CSG_ERR_INVALID, "upload_texture: bad arguments");
+  if (c->textures.size() <= tex_id) c->textures.resize(tex_id + 1);
+  HostTexture& t = c->textures[tex_id];
+  t.rgba.assign(rgba8, rgba8 + (size_t)w * h * 4);
+  t.w = w;
+  t.h = h;
+  t.present = true;
+  c->tex_dirty = true;
+  return CSG_OK;
+}
+
+int csg_set_light(csg_ctx* c, const csg_light* L) {
+  if (!c || !L) return CSG_ERR_INVALID;
+  for (int k = 0; k < 3; ++k) {
+    c->ambient[k] = L->ambient[k];
+    c->sun[k] = L->sun[k];
+    c->sun_dir[k] = L->sun_dir[k];
+  }
+  c->sky = (uint32_t)L->sky[0] | ((uint32_t)L->sky[1] << 8) | ((uint32_t)L->sky[2] << 16);
+  return CSG_OK;
+}
+
+int csg_set_instance_transforms(csg_ctx* c, uint32_t set_id, const float* model4x4, uint32_t n) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "set_instance_transforms: no scene");
+  if (!model4x4 || n != c->n_inst || set_id >= 4096)
+    return c->fail(CSG_ERR_INVALID, "set_instance_transforms: need %u matrices, set < 4096", c->n_inst);
+  const size_t per = (size_t)c->n_inst * 16;
+  if (c->set_valid.size() <= set_id) {
+    c->set_valid.resize(set_id + 1, 0);
+    c->h_models.resize(c->set_valid.size() * per, 0.f);
+  }
+  memcpy(&c->h_models[set_id * per], model4x4, per * sizeof(float));
+  c->set_valid[set_id] = 1;
+  c->models_dirty = true;
+  return CSG_OK;
+}
+
+int csg_set_keypoints(csg_ctx* c, uint32_t set_id, const float* pts, uint32_t n) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!pts || set_id >= 4096 || n == 0) return c->fail(CSG_ERR_INVALID, "set_keypoints: bad arguments");
+  if (c->n_kp && n != c->n_kp) return c->fail(CSG_ERR_INVALID, "set_keypoints: K must stay %u", c->n_kp);
+  c->n_kp = n;
+  if (c->kp_valid.size() <= set_id) {
+    c->kp_valid.resize(set_id + 1, 0);
+    c->h_kp.resize(c->kp_valid.size() * (size_t)n * 3, 0.f);
+  }
+  memcpy(&c->h_kp[(size_t)set_id * n * 3], pts, (size_t)n * 3 * sizeof(float));
+  c->kp_valid[set_id] = 1;
+  c->kp_dirty = true;
+  return CSG_OK;
+}
+
+static int sync_scene_state(csg_ctx* c) {
+  if (c->tex_dirty) {
+    std::vector<TexDesc> td(c->textures.size());
+    size_t total = 0;
+    for (size_t k = 0; k < c->textures.size(); ++k) {
+      td[k] = TexDesc{(uint32_t)total, c->textures[k].w, c->textures[k].h, 0};
+      total += (size_t)c->textures[k].w * c->textures[k].h;
+    }
+    HIP_TRY(c, c->texels.alloc(std::max<size_t>(total * 4, 4)));
+    HIP_TRY(c, c->texd.alloc(std::max<size_t>(td.size(), 1)));
+    for (size_t k = 0; k < c->textures.size(); ++k)
+      if (c->textures[k].present)
+        HIP_TRY(c, hipMemcpy(c->texels.p + (size_t)td[k].offset * 4, c->textures[k].rgba.data(),
+                             c->textures[k].rgba.size(), hipMemcpyHostToDevice));
+    if (!td.empty()) HIP_TRY(c, hipMemcpy(c->texd.p, td.data(), td.size() * sizeof(TexDesc), hipMemcpyHostToDevice));
+    c->tex_dirty = false;
+  }
+  for (uint32_t m = 0; m < c->n_materials; ++m) {
+    const int t = c->h_mats[m].texture;
+    if (t >= 0 && ((size_t)t >= c->textures.size() || !c->textures[t].present))
+      return c->fail(CSG_ERR_INVALID, "material %u references texture %d that was not uploaded", m, t);
+  }
+  if (c->models_dirty) {
+    HIP_TRY(c, c->models.alloc(c->h_models.size()));
+    HIP_TRY(c, hipMemcpy(c->models.p, c->h_models.data(), c->h_models.size() * 4, hipMemcpyHostToDevice));
+    c->models_dirty = false;
+  }
+  if (c->kp_dirty && c->n_kp) {
+    HIP_TRY(c, c->kp.alloc(c->h_kp.size()));
+    HIP_TRY(c, hipMemcpy(c->kp.p, c->h_kp.data(), c->h_kp.size() * 4, hipMemcpyHostToDevice));
+    c->kp_dirty = false;
+  }
+  return CSG_OK;
+}
+
+static int ensure_work(csg_ctx* c, uint32_t F) {
+  const uint32_t maxF = c->cfg.max_frames;
+  if (c->work_frames == maxF && c->rec_cap) return CSG_OK;
+  if (!c->rec_cap) {
+    c->rec_cap = c->cfg.records_per_frame ? c->cfg.records_per_frame
+                                          : (uint32_t)std::min<uint64_t>(c->n_tris_total + c->n_tris_total / 8 + 4096,
+                                                                         0x7FFFFFFFull);
+    c->bin_cap = c->cfg.bins_per_frame ? c->cfg.bins_per_frame
+                                       : (uint32_t)std::min<uint64_t>(3ull * c->rec_cap + 16ull * c->n_tiles,
+                                                                      0x7FFFFFFFull);
+  }
+  const size_t npx = (size_t)c->cfg.width * c->cfg.height;
+  HIP_TRY(c, c->frames.alloc(maxF));
+  if (!c->h_frames) HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_frames), sizeof(FrameDev) * maxF));
+  HIP_TRY(c, c->clip.alloc((size_t)maxF * c->n_inst * 12));
+  HIP_TRY(c, c->pv.alloc((size_t)maxF * 12));
+  HIP_TRY(c, c->recs.alloc((size_t)maxF * c->rec_cap));
+  HIP_TRY(c, c->rect.alloc((size_t)maxF * c->rec_cap));
+  HIP_TRY(c, c->rec_count.alloc(maxF));
+  HIP_TRY(c, c->tile_count.alloc((size_t)maxF * c->n_tiles));
+  HIP_TRY(c, c->tile_off.alloc((size_t)maxF * (c->n_tiles + 1)));
+  HIP_TRY(c, c->tile_fill.alloc((size_t)maxF * c->n_tiles));
+  HIP_TRY(c, c->bins.alloc((size_t)maxF * c->bin_cap));
+  HIP_TRY(c, c->overflow.alloc(1));
+  (void)npx;
+  c->work_frames = maxF;
+  return CSG_OK;
+}
+
+static SceneDev scene_dev(const csg_ctx* c) {
+  SceneDev s{};
+  s.pos = c->pos.p; s.tris = c->tris.p; s.uvs = c->uvs.p; s.uv_tris = c->uv_tris.p;
+  s.meshes = c->meshes.p; s.mats = c->mats.p; s.texd = c->texd.p; s.texels = c->texels.p;
+  s.inst_mesh = c->inst_mesh.p; s.inst_label = c->inst_label.p; s.n_inst = c->n_inst;
+  for (int k = 0; k < 3; ++k) { s.ambient[k] = c->ambient[k]; s.sun[k] = c->sun[k]; s.sun_dir[k] = c->sun_dir[k]; }
+  s.sky = c->sky;
+  s.W = c->cfg.width; s.H = c->cfg.height;
+  s.tiles_x = c->tiles_x; s.tiles_y = c->tiles_y; s.n_tiles = c->n_tiles;
+  s.near_clip = c->cfg.near_clip; s.far_clip = c->cfg.far_clip;
+  return s;
+}
+
+static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int frames_on_device, const csg_outputs* out,
+                         hipStream_t st) {
+  if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "render: no scene uploaded");
+  if (!frames || !out || F == 0 || F > c->cfg.max_frames)
+    return c->fail(CSG_ERR_INVALID, "render: need 1..%u frames", c->cfg.max_frames);
+  int rc = sync_scene_state(c);
+  if (rc) return rc;
+  rc = ensure_work(c, F);
+  if (rc) return rc;
+  const size_t npx = (size_t)c->cfg.width * c->cfg.height;
+  const bool dev = out->on_device != 0;
+  const bool want_kp = c->n_kp && (out->keypoints_uv || out->keypoints_vis);
+  if (!frames_on_device) {
+    for (uint32_t f = 0; f < F; ++f) {
+      const uint32_t set = frames[f].xform_set;
+      if (set >= c->set_valid.size() || !c->set_valid[set])
+        return c->fail(CSG_ERR_INVALID, "frame %u: transform set %u not uploaded", f, set);
+      if (want_kp && (set >= c->kp_valid.size() || !c->kp_valid[set]))
+        return c->fail(CSG_ERR_INVALID, "frame %u: keypoint set %u not uploaded", f, set);
+    }
+  }
+  BatchDev b{};
+  const FrameDev* dframes;
+  if (frames_on_device) {
+    dframes = reinterpret_cast<const FrameDev*>(frames);
+  } else {
+    static_assert(sizeof(FrameDev) == sizeof(csg_frame), "frame layout");
+    memcpy(c->h_frames, frames, sizeof(FrameDev) * F);
+    HIP_TRY(c, hipMemcpyAsync(c->frames.p, c->h_frames, sizeof(FrameDev) * F, hipMemcpyHostToDevice, st));
+    dframes = c->frames.p;
+  }
+  b.frames = dframes;
+  b.models = c->models.p;
+  b.clip = c->clip.p;
+  b.pv = c->pv.p;
+  b.recs = c->recs.p;
+  b.rect = c->rect.p;
+  b.rec_cap = c->rec_cap;
+  b.rec_count = c->rec_count.p;
+  b.tile_count = c->tile_count.p;
+  b.tile_off = c->tile_off.p;
+  b.tile_fill = c->tile_fill.p;
+  b.bins = c->bins.p;
+  b.bin_cap = c->bin_cap;
+  b.overflow = c->overflow.p;
+  b.n_labels = out->n_labels;
+  b.kp = c->kp.p;
+  b.n_kp = want_kp ? c->n_kp : 0;
+  if (dev) {
+    b.rgb = out->rgb;
+    b.inst = out->instance;
+    b.depth = out->depth;
+    b.stats = out->inst_stats;
+    b.kp_uv = out->keypoints_uv;
+    b.kp_vis = out->keypoints_vis;
+  } else {
+    if (out->rgb) { HIP_TRY(c, c->o_rgb.alloc(F * npx * 3)); b.rgb = c->o_rgb.p; }
+    if (out->instance) { HIP_TRY(c, c->o_inst.alloc(F * npx)); b.inst = c->o_inst.p; }
+    if (out->depth) { HIP_TRY(c, c->o_depth.alloc(F * npx)); b.depth = c->o_depth.p; }
+    if (out->inst_stats && out->n_labels) {
+      HIP_TRY(c, c->o_stats.alloc((size_t)F * out->n_labels * 5));
+      b.stats = c->o_stats.p;
+    }
+  }
+  if (!out->inst_stats) b.stats = nullptr;
+  if (want_kp) {
+    if (!b.depth) { HIP_TRY(c, c->o_depth.alloc(F * npx)); b.depth = c->o_depth.p; }
+    if (!b.kp_uv) { HIP_TRY(c, c->o_kp_uv.alloc((size_t)F * c->n_kp * 2)); b.kp_uv = c->o_kp_uv.p; }
+    if (!b.kp_vis) { HIP_TRY(c, c->o_kp_vis.alloc((size_t)F * c->n_kp)); b.kp_vis = c->o_kp_vis.p; }
+  }
+  SceneDev s = scene_dev(c);
+  HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * F, st));
+  HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
+  HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
+  HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), st));
+  launch_init_stats(b, F, st);
+  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[0], st));
+  launch_clip(s, b, F, st);
+  launch_setup(s, b, c->chunks.p, c->n_chunks, F, st);
+  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
+  launch_scan(s, b, F, st);
+  launch_bin(s, b, F, st);
+  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
+  launch_raster(s, b, F, st);
+  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
+  launch_keypoints(s, b, F, st);
+  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
+  HIP_TRY(c, hipGetLastError());
+  c->last_F = F;
+  if (!dev) {
+    if (out->rgb) HIP_TRY(c, hipMemcpyAsync(out->rgb, b.rgb, F * npx * 3, hipMemcpyDeviceToHost, st));
+    if (out->instance) HIP_TRY(c, hipMemcpyAsync(out->instance, b.inst, F * npx * 4, hipMemcpyDeviceToHost, st));
+    if (out->depth) HIP_TRY(c, hipMemcpyAsync(out->depth, b.depth, F * npx * 4, hipMemcpyDeviceToHost, st));
+    if (b.stats)
+      HIP_TRY(c, hipMemcpyAsync(out->inst_stats, b.stats, (size_t)F * out->n_labels * 5 * 4, hipMemcpyDeviceToHost, st));
+    if (want_kp && out->keypoints_uv)
+      HIP_TRY(c, hipMemcpyAsync(out->keypoints_uv, b.kp_uv, (size_t)F * c->n_kp * 8, hipMemcpyDeviceToHost, st));
+    if (want_kp && out->keypoints_vis)
+      HIP_TRY(c, hipMemcpyAsync(out->keypoints_vis, b.kp_vis, (size_t)F * c->n_kp * 4, hipMemcpyDeviceToHost, st));
+  }
+  return CSG_OK;
+}
+
+int csg_render_batch_async(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, int32_t frames_on_device,
+                           const csg_outputs* out, void* stream) {
+  if (!c) return CSG_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+  return enqueue_batch(c, frames, n_frames, frames_on_device, out, st);
+}
+
+int csg_synchronize(csg_ctx* c) {
+  if (!c) return CSG_ERR_INVALID;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  uint32_t ov = 0;
+  if (c->overflow.p) HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
+  if (ov)
+    return c->fail(CSG_ERR_OVERFLOW, "work buffer overflow (flags %u): records_per_frame=%u bins_per_frame=%u", ov,
+                   c->rec_cap, c->bin_cap);
+  return CSG_OK;
+}
+
+int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out) {
+  if (!c) return CSG_ERR_INVALID;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    int rc = csg_render_batch_async(c, frames, n_frames, 0, out, nullptr);
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    uint32_t ov = 0;
+    HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
+    if (!ov) return CSG_OK;
+    // grow the overflowed capacity and re-render (results are a pure function of inputs)
+    if (ov & 1u) c->rec_cap = (uint32_t)std::min<uint64_t>(2ull * c->rec_cap, 0x7FFFFFFFull);
+    if (ov & 2u) c->bin_cap = (uint32_t)std::min<uint64_t>(2ull * c->bin_cap, 0x7FFFFFFFull);
+    c->work_frames = 0;
+  }
+  return c->fail(CSG_ERR_OVERFLOW, "work buffers overflowed after growth");
+}
+
+int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
+  if (!c || !st) return CSG_ERR_INVALID;
+  memset(st, 0, sizeof(*st));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const uint32_t F = c->last_F;
+  if (!F) return CSG_OK;
+  std::vector<uint32_t> rc(F), to((size_t)F * (c->n_tiles + 1));
+  HIP_TRY(c, hipMemcpy(rc.data(), c->rec_count.p, F * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(to.data(), c->tile_off.p, to.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t f = 0; f < F; ++f) {
+    st->records += std::min(rc[f], c->rec_cap);
+    st->bin_entries += to[(size_t)f * (c->n_tiles + 1) + c->n_tiles];
+  }
+  if (c->timing) {
+    float a = 0, b = 0, d = 0, e = 0;
+    HIP_TRY(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    HIP_TRY(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+    HIP_TRY(c, hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
+    HIP_TRY(c, hipEventElapsedTime(&e, c->ev[3], c->ev[4]));
+    st->ms_setup = a;
+    st->ms_bin = b;
+    st->ms_raster = d;
+    st->ms_keypoints = e;
+    st->ms_total = a + b + d + e;
+  }
+  return CSG_OK;
+}
+
+int csg_project_keypoints(csg_ctx* c, const float* pts, uint32_t n, const float* view, const float* proj, float* uv_out,
+                          int32_t* vis_out) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!pts || !view || !proj || !uv_out || !vis_out || n == 0)
+    return c->fail(CSG_ERR_INVALID, "project_keypoints: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  // P*V rows 0,1,3 with the spec's fp32 summation order (host side; 48 products)
+  float pv[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      volatile float t0 = proj[i * 4 + 0] * view[0 * 4 + j];
+      volatile float t1 = proj[i * 4 + 1] * view[1 * 4 + j];
+      volatile float s01 = t0 + t1;
+      volatile float t2 = proj[i * 4 + 2] * view[2 * 4 + j];
+      volatile float s012 = s01 + t2;
+      volatile float t3 = proj[i * 4 + 3] * view[3 * 4 + j];
+      pv[i * 4 + j] = s012 + t3;
+    }
+  float pv12[12];
+  for (int k = 0; k < 4; ++k) { pv12[k] = pv[k]; pv12[4 + k] = pv[4 + k]; pv12[8 + k] = pv[12 + k]; }
+  DevBuf<float> dp, dpv, duv;
+  DevBuf<int32_t> dvis;
+  HIP_TRY(c, dp.alloc((size_t)n * 3));
+  HIP_TRY(c, dpv.alloc(12));
+  HIP_TRY(c, duv.alloc((size_t)n * 2));
+  HIP_TRY(c, dvis.alloc(n));
+  HIP_TRY(c, hipMemcpy(dp.p, pts, (size_t)n * 12, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(dpv.p, pv12, 48, hipMemcpyHostToDevice));
+  launch_project(dp.p, n, dpv.p, (float)c->cfg.width, (float)c->cfg.height, c->cfg.near_clip, duv.p, dvis.p,
+                 c->stream);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(uv_out, duv.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(vis_out, dvis.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  dp.release(); dpv.release(); duv.release(); dvis.release();
+  return CSG_OK;
+}
+
+}  // extern "C"

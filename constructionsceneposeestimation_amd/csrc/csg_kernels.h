@@ -1,0 +1,100 @@
+// Internal interface between the C-ABI host code (csg_api.cpp) and the
+// gfx950 kernels (csg_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace csg {
+
+constexpr int kTile = 32;                 // screen tile edge (pixels)
+constexpr int kTilePix = kTile * kTile;   // 1024 pixels, one 256-thread workgroup
+constexpr int kBlock = 256;
+constexpr uint32_t kUidShift = 20;        // uid = (instance << 20) | triangle
+constexpr uint32_t kMaxInstances = 1u << (32 - kUidShift);
+constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
+constexpr int kMaxLdsLabels = 256;        // per-label pixel stats kept in LDS
+
+struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };
+struct MatDesc { uint8_t base[4]; int32_t texture; uint32_t alpha_test, alpha_threshold; };
+struct TexDesc { uint32_t offset, width, height, pad; };
+struct Chunk { uint32_t inst, start, count, pad; };   // <= 256 triangles of one instance
+
+// One raster (sub-)triangle: fixed-point screen vertices for coverage plus the
+// homogeneous coefficients of its ORIGINAL triangle for depth/attributes.
+struct __attribute__((aligned(16))) Rec {
+  int32_t x[3], y[3];          // 24: 24.8 fixed point, positive orientation
+  uint16_t px0, py0, px1, py1; // 8 : inclusive pixel bbox, clamped to the frame
+  uint32_t uid;                // 4
+  uint32_t mat;                // 4 : material index
+  float A[3], B[3], C[3];      // 36: e_k = A_k*x + B_k*y + C_k
+  float invdet;                // 4
+  float uv[6];                 // 24: only read for alpha-tested materials
+  uint32_t pad[2];             // 8
+};
+static_assert(sizeof(Rec) == 112, "Rec layout");
+
+struct FrameDev {                // csg_frame mirror
+  float view[16];
+  float proj[16];
+  uint32_t xform_set;
+  uint32_t frame_id;
+};
+
+struct SceneDev {
+  const float* pos;
+  const uint32_t* tris;
+  const float* uvs;
+  const uint32_t* uv_tris;
+  const MeshDesc* meshes;
+  const MatDesc* mats;
+  const TexDesc* texd;
+  const uint8_t* texels;
+  const uint32_t* inst_mesh;
+  const int32_t* inst_label;
+  uint32_t n_inst;
+  float ambient[3], sun[3], sun_dir[3];
+  uint32_t sky;                // packed r | g<<8 | b<<16
+  uint32_t W, H, tiles_x, tiles_y, n_tiles;
+  float near_clip, far_clip;
+};
+
+struct BatchDev {
+  const FrameDev* frames;      // [F]
+  const float* models;         // [n_sets][I][16]
+  float* clip;                 // [F][I][12] rows 0,1,3 of P*V*M
+  float* pv;                   // [F][12]    rows 0,1,3 of P*V
+  Rec* recs;                   // [F][rec_cap]
+  uint32_t* rect;              // [F][rec_cap] tile rect tx0|ty0<<8|tx1<<16|ty1<<24
+  uint32_t rec_cap;
+  uint32_t* rec_count;         // [F]
+  uint32_t* tile_count;        // [F][n_tiles]
+  uint32_t* tile_off;          // [F][n_tiles+1]
+  uint32_t* tile_fill;         // [F][n_tiles]
+  uint32_t* bins;              // [F][bin_cap]
+  uint32_t bin_cap;
+  uint32_t* overflow;          // [1] bit0 rec, bit1 bins
+  // outputs (device)
+  uint8_t* rgb;                // [F][H][W][3] or null
+  int32_t* inst;               // [F][H][W] or null
+  float* depth;                // [F][H][W] (internal scratch when the caller wants none)
+  uint32_t* stats;             // [F][n_labels][5] or null
+  uint32_t n_labels;
+  const float* kp;             // [n_sets][K][3]
+  uint32_t n_kp;
+  float* kp_uv;                // [F][K][2]
+  int32_t* kp_vis;             // [F][K]
+};
+
+// launchers (all enqueue on `st`)
+void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks,
+                  uint32_t F, hipStream_t st);
+void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip,
+                    float* uv, int32_t* vis, hipStream_t st);
+
+}  // namespace csg

@@ -1,0 +1,847 @@
+// gfx950 (MI355X / CDNA4) kernels of the construction-scene frame generator.
+//
+// Replaces the per-frame render + annotate step the reference gets from
+// Isaac Sim RTX + Replicator (generate_construction_data.py:1586-1595 pose +
+// render, :1669 RGB, :1681 depth, :1475/:1909 instance mask, :1780/:1916
+// bounding boxes).  The arithmetic follows DESIGN.md "Raster spec" exactly:
+// this file must stay bit-identical to oracle/csg_oracle.c (built with
+// -ffp-contract=off on both sides; every float expression below is written
+// in the same order as there).
+//
+// Pipeline per batch of F frames (all frames of a batch in every launch):
+//   k_clip     (F x instances)   P*V*M in fp32, fixed summation order
+//   k_setup    (chunks x F)      transform, cull, near-clip, fixed-point
+//                                setup, wave-ballot record append, LDS tile
+//                                histogram -> per-tile counts
+//   k_scan     (F)               exclusive scan of tile counts
+//   k_bin      (64 x F)          LDS-aggregated scatter of record ids to bins
+//   k_raster   (tiles x F)       32x32 tile: bins staged in LDS, balanced
+//                                (record,pixel) expansion, 64-bit
+//                                (depth,uid) z-buffer in LDS (ds_min_u64),
+//                                then resolve: texture, shade, instance id,
+//                                depth, coalesced HBM writes, label stats
+//   k_keypoints(K x F)           3D->2D projection + depth-tested visibility
+#include <math.h>
+
+#include "csg_kernels.h"
+
+namespace csg {
+
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr float kGuardPx = 1048576.0f;
+constexpr int kSmallRect = 8;    // tile rects up to this many tiles are counted per lane
+
+// ---------------------------------------------------------------------------
+// shared arithmetic (mirrors csg_oracle.c line by line)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float dot4(const float* r, float x, float y, float z) {
+  return ((r[0] * x + r[1] * y) + r[2] * z) + r[3];
+}
+
+__device__ __forceinline__ void mat4_mul(const float* a, const float* b, float* c) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      c[i * 4 + j] = ((a[i * 4 + 0] * b[0 * 4 + j] + a[i * 4 + 1] * b[1 * 4 + j]) + a[i * 4 + 2] * b[2 * 4 + j]) +
+                     a[i * 4 + 3] * b[3 * 4 + j];
+}
+
+struct Cv3 { float x, y, w; };
+
+struct Hom {
+  float A[3], B[3], C[3];
+  float invdet;
+  bool ok;
+};
+
+__device__ __forceinline__ void hom_setup(const Cv3* v, Hom& h) {
+  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const Cv3 a = v[ea[k]], b = v[eb[k]];
+    h.A[k] = a.y * b.w - a.w * b.y;
+    h.B[k] = a.w * b.x - a.x * b.w;
+    h.C[k] = a.x * b.y - a.y * b.x;
+  }
+  const float det = (v[0].x * h.A[0] + v[0].y * h.B[0]) + v[0].w * h.C[0];
+  h.ok = det != 0.0f;
+  h.invdet = h.ok ? 1.0f / det : 0.0f;
+}
+
+__device__ __forceinline__ void hom_eval(const float* A, const float* B, const float* C, float invdet, int px, int py,
+                                         float* e, float& ssum, float& invw) {
+  const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) e[k] = (A[k] * fx + B[k] * fy) + C[k];
+  ssum = (e[0] + e[1]) + e[2];
+  invw = ssum * invdet;
+}
+
+__device__ __forceinline__ void interp_uv(const float* e, float ssum, const float* uv, float& u, float& v) {
+  const float rs = 1.0f / ssum;
+  const float l0 = e[0] * rs, l1 = e[1] * rs, l2 = e[2] * rs;
+  u = (l0 * uv[0] + l1 * uv[2]) + l2 * uv[4];
+  v = (l0 * uv[1] + l1 * uv[3]) + l2 * uv[5];
+}
+
+// Bilinear RGBA8, repeat wrap, 8-bit fixed weights. `only_alpha` skips RGB.
+__device__ __forceinline__ void tex_sample(const SceneDev& s, int tid, float u, float v, int out[4]) {
+  const TexDesc t = s.texd[tid];
+  const int tw = (int)t.width, th = (int)t.height;
+  float tu = u * (float)tw - 0.5f;
+  float tv = (1.0f - v) * (float)th - 0.5f;
+  if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
+  if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
+  const float fu = floorf(tu), fv = floorf(tv);
+  const int wx = (int)((tu - fu) * 256.0f), wy = (int)((tv - fv) * 256.0f);
+  int x0 = (int)fu % tw;
+  if (x0 < 0) x0 += tw;
+  int y0 = (int)fv % th;
+  if (y0 < 0) y0 += th;
+  const int x1 = (x0 + 1 == tw) ? 0 : x0 + 1;
+  const int y1 = (y0 + 1 == th) ? 0 : y0 + 1;
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(s.texels) + t.offset;
+  const uint32_t c00 = base[(size_t)y0 * tw + x0], c10 = base[(size_t)y0 * tw + x1];
+  const uint32_t c01 = base[(size_t)y1 * tw + x0], c11 = base[(size_t)y1 * tw + x1];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int sh = 8 * c;
+    const int top = (int)((c00 >> sh) & 255u) * (256 - wx) + (int)((c10 >> sh) & 255u) * wx;
+    const int bot = (int)((c01 >> sh) & 255u) * (256 - wx) + (int)((c11 >> sh) & 255u) * wx;
+    out[c] = (top * (256 - wy) + bot * wy + 32768) >> 16;
+  }
+}
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+
+// ---------------------------------------------------------------------------
+// wave / block helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t n = __shfl_up(v, d, 64);
+    if (lane >= d) v += n;
+  }
+  return v;
+}
+
+// exclusive scan over the 256-thread block; `wsum` is LDS[4]
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+  const uint32_t inc = wave_incl_scan(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / 64; ++k) {
+    const uint32_t x = wsum[k];
+    off += (k < w) ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return off + inc - v;
+}
+
+// last k in [0,256) with pre[k] <= j  (pre has 257 entries, j < pre[256])
+__device__ __forceinline__ int find_item(const uint32_t* pre, uint32_t j) {
+  int lo = 0;
+#pragma unroll
+  for (int step = 128; step > 0; step >>= 1)
+    if (pre[lo + step] <= j) lo += step;
+  return lo;
+}
+
+// ---------------------------------------------------------------------------
+// k_clip: per (frame, instance) clip rows of P*V*M; per frame P*V
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_clip(SceneDev s, BatchDev b) {
+  const uint32_t f = blockIdx.y;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const FrameDev& fr = b.frames[f];
+  if (i < s.n_inst) {
+    const float* M = b.models + ((size_t)fr.xform_set * s.n_inst + i) * 16;
+    float m[16], vm[16], c[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = M[k];
+    mat4_mul(fr.view, m, vm);
+    mat4_mul(fr.proj, vm, c);
+    float* o = b.clip + ((size_t)f * s.n_inst + i) * 12;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = c[k];
+      o[4 + k] = c[4 + k];
+      o[8 + k] = c[12 + k];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float pv[16];
+    mat4_mul(fr.proj, fr.view, pv);
+    float* o = b.pv + (size_t)f * 12;
+    for (int k = 0; k < 4; ++k) {
+      o[k] = pv[k];
+      o[4 + k] = pv[4 + k];
+      o[8 + k] = pv[12 + k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_setup
+// ---------------------------------------------------------------------------
+// Build one raster record from screen-space vertices; false if it covers no pixel.
+__device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, const float* sv, Rec& r) {
+  int32_t x[3], y[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (!(fabsf(su[k]) < kGuardPx) || !(fabsf(sv[k]) < kGuardPx)) return false;
+    x[k] = (int32_t)rintf(su[k] * 256.0f);
+    y[k] = (int32_t)rintf(sv[k] * 256.0f);
+  }
+  const int64_t area = (int64_t)(x[1] - x[0]) * (y[2] - y[0]) - (int64_t)(x[2] - x[0]) * (y[1] - y[0]);
+  if (area == 0) return false;
+  if (area < 0) {
+    int32_t t = x[1]; x[1] = x[2]; x[2] = t;
+    t = y[1]; y[1] = y[2]; y[2] = t;
+  }
+  const int32_t xmin = min(x[0], min(x[1], x[2])), xmax = max(x[0], max(x[1], x[2]));
+  const int32_t ymin = min(y[0], min(y[1], y[2])), ymax = max(y[0], max(y[1], y[2]));
+  int px0 = (xmin - 128 + 255) >> 8, px1 = (xmax - 128) >> 8;
+  int py0 = (ymin - 128 + 255) >> 8, py1 = (ymax - 128) >> 8;
+  px0 = max(px0, 0);
+  py0 = max(py0, 0);
+  px1 = min(px1, (int)s.W - 1);
+  py1 = min(py1, (int)s.H - 1);
+  if (px0 > px1 || py0 > py1) return false;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { r.x[k] = x[k]; r.y[k] = y[k]; }
+  r.px0 = (uint16_t)px0; r.py0 = (uint16_t)py0; r.px1 = (uint16_t)px1; r.py1 = (uint16_t)py1;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t rec_tile_rect(const Rec& r) {
+  return (uint32_t)(r.px0 / kTile) | ((uint32_t)(r.py0 / kTile) << 8) | ((uint32_t)(r.px1 / kTile) << 16) |
+         ((uint32_t)(r.py1 / kTile) << 24);
+}
+
+__device__ __forceinline__ void store_rec(Rec* dst, const Rec& r) {
+  const uint4* src = reinterpret_cast<const uint4*>(&r);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) d[k] = src[k];
+}
+
+__device__ __forceinline__ uint32_t rect_area(uint32_t rc) {
+  const uint32_t tx0 = rc & 255u, ty0 = (rc >> 8) & 255u, tx1 = (rc >> 16) & 255u, ty1 = rc >> 24;
+  return (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+}
+
+__device__ __forceinline__ uint32_t rect_tile(uint32_t rc, uint32_t q, uint32_t tiles_x) {
+  const uint32_t tx0 = rc & 255u, ty0 = (rc >> 8) & 255u, tx1 = (rc >> 16) & 255u;
+  const uint32_t w = tx1 - tx0 + 1;
+  return (ty0 + q / w) * tiles_x + tx0 + q % w;
+}
+
+__global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chunk* __restrict__ chunks) {
+  extern __shared__ uint32_t hist[];                 // [n_tiles]
+  __shared__ uint32_t big[2 * kBlock];
+  __shared__ uint32_t n_big;
+  const uint32_t f = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const Chunk ch = chunks[blockIdx.x];
+  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
+  if (tid == 0) n_big = 0;
+
+  Rec r0, r1;   // named, never runtime-indexed (a Rec[2] would live in scratch)
+  int nrec = 0;
+  const uint32_t i = ch.inst;
+  if ((uint32_t)tid < ch.count) {
+    const uint32_t t = ch.start + tid;
+    const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
+    float c[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) c[k] = Cm[k];
+    const MeshDesc m = s.meshes[s.inst_mesh[i]];
+    const uint32_t* tri = s.tris + (size_t)(m.tbase + t) * 3;
+    Cv3 v[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float* p = s.pos + (size_t)(m.vbase + tri[k]) * 3;
+      const float px = p[0], py = p[1], pz = p[2];
+      v[k].x = dot4(c + 0, px, py, pz);
+      v[k].y = dot4(c + 4, px, py, pz);
+      v[k].w = dot4(c + 8, px, py, pz);
+    }
+    const float nearc = s.near_clip, farc = s.far_clip;
+    const float Wf = (float)s.W, Hf = (float)s.H;
+    bool on = true, of = true, ol = true, orr = true, ot = true, ob = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      on &= v[k].w < nearc;
+      of &= v[k].w > farc;
+      ol &= v[k].x < 0.0f;
+      orr &= v[k].x > Wf * v[k].w;
+      ot &= v[k].y < 0.0f;
+      ob &= v[k].y > Hf * v[k].w;
+    }
+    Hom h;
+    if (!(on | of | ol | orr | ot | ob)) {
+      hom_setup(v, h);
+      if (h.ok) {
+        const MatDesc mat = s.mats[m.material];
+        float uv[6] = {0, 0, 0, 0, 0, 0};
+        if (mat.alpha_test && m.has_uv) {
+          const uint32_t* ut = s.uv_tris + (size_t)(m.tbase + t) * 3;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const float* q = s.uvs + (size_t)(m.uvbase + ut[k]) * 2;
+            uv[2 * k] = q[0];
+            uv[2 * k + 1] = q[1];
+          }
+        }
+        const uint32_t uid = (i << kUidShift) | t;
+        // Sutherland-Hodgman against W >= near over edges v0->v1, v1->v2, v2->v0
+        // (each edge emits [start vertex if inside][intersection if crossing]),
+        // written as a closed-form case table on the inside mask so the polygon
+        // stays in registers.
+        Cv3 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[2];
+        int nq = 3;
+        const bool in0 = v[0].w >= nearc, in1 = v[1].w >= nearc, in2 = v[2].w >= nearc;
+        if (!(in0 && in1 && in2)) {
+          auto cross_pt = [&](const Cv3& a, const Cv3& bb) {
+            const float tt = (nearc - a.w) / (bb.w - a.w);
+            Cv3 rr;
+            rr.x = a.x + tt * (bb.x - a.x);
+            rr.y = a.y + tt * (bb.y - a.y);
+            rr.w = nearc;
+            return rr;
+          };
+          auto sel = [](bool c, const Cv3& a, const Cv3& bb) {
+            Cv3 rr;
+            rr.x = c ? a.x : bb.x;
+            rr.y = c ? a.y : bb.y;
+            rr.w = c ? a.w : bb.w;
+            return rr;
+          };
+          const Cv3 I01 = cross_pt(v[0], v[1]), I12 = cross_pt(v[1], v[2]), I20 = cross_pt(v[2], v[0]);
+          const int code = (int)in0 | ((int)in1 << 1) | ((int)in2 << 2);
+          // code: 1 -> v0 I01 I20 | 2 -> I01 v1 I12 | 4 -> I12 v2 I20
+          //       3 -> v0 v1 I12 I20 | 6 -> I01 v1 v2 I20 | 5 -> v0 I01 I12 v2
+          q0 = sel(code == 2 || code == 6, I01, sel(code == 4, I12, v[0]));
+          q1 = sel(code == 1 || code == 5, I01, sel(code == 4, v[2], v[1]));
+          q2 = sel(code == 1 || code == 4, I20, sel(code == 6, v[2], I12));
+          q3 = sel(code == 3 || code == 6, I20, v[2]);
+          nq = (code == 1 || code == 2 || code == 4) ? 3 : 4;
+        }
+        auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
+          float su[3], sv[3];
+          su[0] = a.x / a.w; sv[0] = a.y / a.w;
+          su[1] = bb.x / bb.w; sv[1] = bb.y / bb.w;
+          su[2] = cc.x / cc.w; sv[2] = cc.y / cc.w;
+          Rec rr;
+          if (make_rec(s, su, sv, rr)) {
+            rr.uid = uid;
+            rr.mat = m.material;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { rr.A[k] = h.A[k]; rr.B[k] = h.B[k]; rr.C[k] = h.C[k]; }
+            rr.invdet = h.invdet;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) rr.uv[k] = uv[k];
+            rr.pad[0] = rr.pad[1] = 0;
+            if (nrec == 0) r0 = rr; else r1 = rr;
+            ++nrec;
+          }
+        };
+        if (nq >= 3) emit_tri(q0, q1, q2);
+        if (nq >= 4) emit_tri(q0, q2, q3);
+      }
+    }
+  }
+  // wave-ballot compaction of the emitted records into the frame's record list
+  const uint64_t b1 = __ballot(nrec >= 1), b2 = __ballot(nrec >= 2);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t mine = (uint32_t)(__popcll(b1 & lt) + __popcll(b2 & lt));
+  const uint32_t wtot = (uint32_t)(__popcll(b1) + __popcll(b2));
+  uint32_t wbase = 0;
+  if (lane == 0 && wtot) wbase = atomicAdd(&b.rec_count[f], wtot);
+  wbase = __shfl(wbase, 0, 64);
+  __syncthreads();   // hist zeroed
+  auto emit = [&](const Rec& rec, uint32_t slot) {
+    if (slot >= b.rec_cap) {
+      atomicOr(b.overflow, 1u);
+      return;
+    }
+    store_rec(b.recs + (size_t)f * b.rec_cap + slot, rec);
+    const uint32_t rc = rec_tile_rect(rec);
+    b.rect[(size_t)f * b.rec_cap + slot] = rc;
+    const uint32_t area = rect_area(rc);
+    if (area <= (uint32_t)kSmallRect) {
+      for (uint32_t q = 0; q < area; ++q) atomicAdd(&hist[rect_tile(rc, q, s.tiles_x)], 1u);
+    } else {
+      big[atomicAdd(&n_big, 1u)] = rc;
+    }
+  };
+  if (nrec > 0) emit(r0, wbase + mine);
+  if (nrec > 1) emit(r1, wbase + mine + 1);
+  __syncthreads();
+  const uint32_t nb = n_big;
+  for (uint32_t e = 0; e < nb; ++e) {
+    const uint32_t rc = big[e];
+    const uint32_t area = rect_area(rc);
+    for (uint32_t q = tid; q < area; q += kBlock) atomicAdd(&hist[rect_tile(rc, q, s.tiles_x)], 1u);
+  }
+  __syncthreads();
+  uint32_t* tc = b.tile_count + (size_t)f * s.n_tiles;
+  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) {
+    const uint32_t c = hist[t];
+    if (c) atomicAdd(&tc[t], c);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_scan: per frame exclusive scan of tile counts (one 256-thread block)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_scan(SceneDev s, BatchDev b) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t carry;
+  const uint32_t f = blockIdx.x;
+  const uint32_t* tc = b.tile_count + (size_t)f * s.n_tiles;
+  uint32_t* to = b.tile_off + (size_t)f * (s.n_tiles + 1);
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < s.n_tiles; base += kBlock) {
+    const uint32_t t = base + threadIdx.x;
+    const uint32_t v = t < s.n_tiles ? tc[t] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(v, wsum, tot);
+    const uint32_t c0 = carry;
+    if (t < s.n_tiles) to[t] = c0 + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) carry = c0 + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    to[s.n_tiles] = carry;
+    if (carry > b.bin_cap) atomicOr(b.overflow, 2u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_bin: scatter record ids into per-tile bins (LDS-aggregated atomics)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
+  extern __shared__ uint32_t dyn[];
+  uint32_t* hist = dyn;                  // [n_tiles]
+  uint32_t* tbase = dyn + s.n_tiles;     // [n_tiles]
+  __shared__ uint32_t pre[kBlock + 1];
+  __shared__ uint32_t lrc[kBlock];
+  __shared__ uint32_t wsum[kBlock / 64];
+  const uint32_t f = blockIdx.y;
+  const int tid = threadIdx.x;
+  const uint32_t n = min(b.rec_count[f], b.rec_cap);
+  const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
+  const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
+  uint32_t* fill = b.tile_fill + (size_t)f * s.n_tiles;
+  uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
+  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
+  __syncthreads();
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t r = base + tid;
+    uint32_t area = 0;
+    if (r < n) {
+      const uint32_t rc = rect[r];
+      lrc[tid] = rc;
+      area = rect_area(rc);
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(area, wsum, total);
+    pre[tid] = ex;
+    if (tid == kBlock - 1) pre[kBlock] = ex + area;
+    __syncthreads();
+    for (uint32_t j = tid; j < total; j += kBlock) {
+      const int k = find_item(pre, j);
+      atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < s.n_tiles; t += kBlock) {
+      const uint32_t c = hist[t];
+      if (c) {
+        tbase[t] = toff[t] + atomicAdd(&fill[t], c);
+        hist[t] = 0;
+      }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < total; j += kBlock) {
+      const int k = find_item(pre, j);
+      const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
+      const uint32_t slot = tbase[t] + atomicAdd(&hist[t], 1u);
+      if (slot < b.bin_cap) bins[slot] = base + (uint32_t)k;
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_raster: one 32x32 tile of one frame per 256-thread workgroup
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
+  __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
+  __shared__ Rec lrec[kBlock];                       // 28 KiB staged bin records
+  __shared__ uint32_t lrect[kBlock];
+  __shared__ uint32_t pre[kBlock + 1];
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t lstat[5][kMaxLdsLabels];
+  const int tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x, f = blockIdx.y;
+  const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
+  for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
+  const uint32_t nl = min(b.n_labels, (uint32_t)kMaxLdsLabels);
+  for (uint32_t l = tid; l < nl; l += kBlock) {
+    lstat[0][l] = 0; lstat[1][l] = 0xFFFFFFFFu; lstat[2][l] = 0xFFFFFFFFu; lstat[3][l] = 0; lstat[4][l] = 0;
+  }
+  const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
+  const uint32_t beg = min(toff[tile], b.bin_cap), end = min(toff[tile + 1], b.bin_cap);
+  const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
+  const Rec* recs = b.recs + (size_t)f * b.rec_cap;
+  const float inv_near = 1.0f / s.near_clip, inv_far = 1.0f / s.far_clip;
+  __syncthreads();
+
+  for (uint32_t base = beg; base < end; base += kBlock) {
+    const uint32_t idx = base + tid;
+    uint32_t area = 0;
+    const uint32_t r = (idx < end) ? bins[idx] : 0xFFFFFFFFu;
+    if (r < b.rec_cap) {
+      const uint4* src = reinterpret_cast<const uint4*>(recs + r);
+      uint4* dst = reinterpret_cast<uint4*>(&lrec[tid]);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) dst[k] = src[k];
+      const Rec& R = lrec[tid];
+      const int x0 = max((int)R.px0, ox) - ox, x1 = min((int)R.px1, ox + kTile - 1) - ox;
+      const int y0 = max((int)R.py0, oy) - oy, y1 = min((int)R.py1, oy + kTile - 1) - oy;
+      if (x0 <= x1 && y0 <= y1) {
+        const uint32_t w = (uint32_t)(x1 - x0 + 1), hh = (uint32_t)(y1 - y0 + 1);
+        area = w * hh;
+        lrect[tid] = (uint32_t)x0 | ((uint32_t)y0 << 8) | (w << 16);
+      }
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(area, wsum, total);
+    pre[tid] = ex;
+    if (tid == kBlock - 1) pre[kBlock] = ex + area;
+    __syncthreads();
+    for (uint32_t j = tid; j < total; j += kBlock) {
+      const int k = find_item(pre, j);
+      const uint32_t q = j - pre[k];
+      const uint32_t rc = lrect[k];
+      const uint32_t w = rc >> 16;
+      const int lx = (int)(rc & 255u) + (int)(q % w), ly = (int)((rc >> 8) & 255u) + (int)(q / w);
+      const int px = ox + lx, py = oy + ly;
+      const Rec& R = lrec[k];
+      const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
+      const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+      bool inside = true;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
+        const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
+        const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+        const int64_t ev = (int64_t)dx * (cy - ay) - (int64_t)dy * (cx - ax);
+        inside &= (ev + bias) >= 0;
+      }
+      if (!inside) continue;
+      float e[3], ssum, invw;
+      hom_eval(R.A, R.B, R.C, R.invdet, px, py, e, ssum, invw);
+      if (!(invw >= inv_far && invw <= inv_near)) continue;
+      const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | R.uid;
+      unsigned long long* z = &zb[ly * kTile + lx];
+      if (key >= *z) continue;
+      const MatDesc mat = s.mats[R.mat];
+      if (mat.alpha_test && mat.texture >= 0) {
+        float u, v;
+        int c[4];
+        interp_uv(e, ssum, R.uv, u, v);
+        tex_sample(s, mat.texture, u, v, c);
+        if (!(c[3] > (int)mat.alpha_threshold)) continue;
+      }
+      atomicMin(z, key);
+    }
+    __syncthreads();
+  }
+
+  // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads
+  const int ly = tid >> 3, lx0 = (tid & 7) * 4;
+  const int py = oy + ly;
+  const size_t npx = (size_t)s.W * s.H;
+  if (py < (int)s.H) {
+    uint8_t rgb[12];
+    int32_t ids[4];
+    float dep[4];
+    uint32_t last_uid = 0xFFFFFFFFu;
+    // cached per-triangle state
+    Hom h;
+    float uvv[6];
+    int32_t label = -1;
+    int alb_const[3] = {0, 0, 0};
+    int tex = -1;
+    uint8_t mbase[3] = {0, 0, 0};
+    int q[3] = {0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int px = ox + lx0 + k;
+      const unsigned long long key = zb[ly * kTile + lx0 + k];
+      if (key == kEmptyKey || px >= (int)s.W) {
+        rgb[3 * k + 0] = (uint8_t)(s.sky & 255u);
+        rgb[3 * k + 1] = (uint8_t)((s.sky >> 8) & 255u);
+        rgb[3 * k + 2] = (uint8_t)((s.sky >> 16) & 255u);
+        ids[k] = -1;
+        dep[k] = INFINITY;
+        continue;
+      }
+      const uint32_t uid = (uint32_t)key;
+      const uint32_t i = uid >> kUidShift, t = uid & (kMaxTrisPerMesh - 1u);
+      if (uid != last_uid) {
+        last_uid = uid;
+        const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
+        float c[12];
+#pragma unroll
+        for (int z = 0; z < 12; ++z) c[z] = Cm[z];
+        const MeshDesc m = s.meshes[s.inst_mesh[i]];
+        const uint32_t* tri = s.tris + (size_t)(m.tbase + t) * 3;
+        float pobj[3][3];
+        Cv3 v[3];
+#pragma unroll
+        for (int z = 0; z < 3; ++z) {
+          const float* p = s.pos + (size_t)(m.vbase + tri[z]) * 3;
+          pobj[z][0] = p[0]; pobj[z][1] = p[1]; pobj[z][2] = p[2];
+          v[z].x = dot4(c + 0, p[0], p[1], p[2]);
+          v[z].y = dot4(c + 4, p[0], p[1], p[2]);
+          v[z].w = dot4(c + 8, p[0], p[1], p[2]);
+        }
+        hom_setup(v, h);
+        label = s.inst_label[i];
+        const MatDesc mat = s.mats[m.material];
+        tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
+        mbase[0] = mat.base[0]; mbase[1] = mat.base[1]; mbase[2] = mat.base[2];
+        if (tex >= 0) {
+          const uint32_t* ut = s.uv_tris + (size_t)(m.tbase + t) * 3;
+#pragma unroll
+          for (int z = 0; z < 3; ++z) {
+            const float* uq = s.uvs + (size_t)(m.uvbase + ut[z]) * 2;
+            uvv[2 * z] = uq[0];
+            uvv[2 * z + 1] = uq[1];
+          }
+        } else {
+          alb_const[0] = mbase[0]; alb_const[1] = mbase[1]; alb_const[2] = mbase[2];
+        }
+        // flat two-sided Lambert from the world-space face normal
+        const float* M = b.models + ((size_t)b.frames[f].xform_set * s.n_inst + i) * 16;
+        float mm[12];
+#pragma unroll
+        for (int z = 0; z < 12; ++z) mm[z] = M[z];
+        float pw[3][3];
+#pragma unroll
+        for (int z = 0; z < 3; ++z) {
+          pw[z][0] = dot4(mm + 0, pobj[z][0], pobj[z][1], pobj[z][2]);
+          pw[z][1] = dot4(mm + 4, pobj[z][0], pobj[z][1], pobj[z][2]);
+          pw[z][2] = dot4(mm + 8, pobj[z][0], pobj[z][1], pobj[z][2]);
+        }
+        const float e1x = pw[1][0] - pw[0][0], e1y = pw[1][1] - pw[0][1], e1z = pw[1][2] - pw[0][2];
+        const float e2x = pw[2][0] - pw[0][0], e2y = pw[2][1] - pw[0][1], e2z = pw[2][2] - pw[0][2];
+        const float nx = e1y * e2z - e1z * e2y;
+        const float ny = e1z * e2x - e1x * e2z;
+        const float nz = e1x * e2y - e1y * e2x;
+        const float nn = (nx * nx + ny * ny) + nz * nz;
+        float cs = 0.0f;
+        if (nn > 0.0f) {
+          const float d = (nx * s.sun_dir[0] + ny * s.sun_dir[1]) + nz * s.sun_dir[2];
+          cs = fabsf(d / sqrtf(nn));
+        }
+#pragma unroll
+        for (int z = 0; z < 3; ++z) {
+          const float shade = s.ambient[z] + s.sun[z] * cs;
+          int qq = (int)(shade * 256.0f + 0.5f);
+          q[z] = min(max(qq, 0), 65535);
+        }
+      }
+      float e[3], ssum, invw;
+      hom_eval(h.A, h.B, h.C, h.invdet, px, py, e, ssum, invw);
+      dep[k] = 1.0f / invw;
+      ids[k] = label;
+      int alb[3];
+      if (tex >= 0) {
+        float u, v;
+        int c[4];
+        interp_uv(e, ssum, uvv, u, v);
+        tex_sample(s, tex, u, v, c);
+#pragma unroll
+        for (int z = 0; z < 3; ++z) alb[z] = (c[z] * mbase[z] + 127) / 255;
+      } else {
+#pragma unroll
+        for (int z = 0; z < 3; ++z) alb[z] = alb_const[z];
+      }
+#pragma unroll
+      for (int z = 0; z < 3; ++z) {
+        const int o = (alb[z] * q[z] + 128) >> 8;
+        rgb[3 * k + z] = (uint8_t)min(o, 255);
+      }
+      if (label >= 0 && (uint32_t)label < nl) {
+        atomicAdd(&lstat[0][label], 1u);
+        atomicMin(&lstat[1][label], (uint32_t)px);
+        atomicMin(&lstat[2][label], (uint32_t)py);
+        atomicMax(&lstat[3][label], (uint32_t)px);
+        atomicMax(&lstat[4][label], (uint32_t)py);
+      }
+    }
+    const int px0 = ox + lx0;
+    const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
+    if (px0 + 3 < (int)s.W) {
+      if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(ids[0], ids[1], ids[2], ids[3]);
+      if (b.depth) *reinterpret_cast<float4*>(b.depth + o) = make_float4(dep[0], dep[1], dep[2], dep[3]);
+      if (b.rgb) {
+        uint32_t w3[3];
+#pragma unroll
+        for (int z = 0; z < 3; ++z)
+          w3[z] = (uint32_t)rgb[4 * z] | ((uint32_t)rgb[4 * z + 1] << 8) | ((uint32_t)rgb[4 * z + 2] << 16) |
+                  ((uint32_t)rgb[4 * z + 3] << 24);
+        uint32_t* d = reinterpret_cast<uint32_t*>(b.rgb + o * 3);
+        d[0] = w3[0]; d[1] = w3[1]; d[2] = w3[2];
+      }
+    } else {
+      for (int k = 0; k < 4 && px0 + k < (int)s.W; ++k) {
+        if (b.inst) b.inst[o + k] = ids[k];
+        if (b.depth) b.depth[o + k] = dep[k];
+        if (b.rgb) {
+          b.rgb[(o + k) * 3 + 0] = rgb[3 * k];
+          b.rgb[(o + k) * 3 + 1] = rgb[3 * k + 1];
+          b.rgb[(o + k) * 3 + 2] = rgb[3 * k + 2];
+        }
+      }
+    }
+  }
+  if (b.stats) {
+    __syncthreads();
+    uint32_t* st = b.stats + (size_t)f * b.n_labels * 5;
+    for (uint32_t l = tid; l < nl; l += kBlock) {
+      const uint32_t c = lstat[0][l];
+      if (c) {
+        atomicAdd(&st[l * 5 + 0], c);
+        atomicMin(&st[l * 5 + 1], lstat[1][l]);
+        atomicMin(&st[l * 5 + 2], lstat[2][l]);
+        atomicMax(&st[l * 5 + 3], lstat[3][l]);
+        atomicMax(&st[l * 5 + 4], lstat[4][l]);
+      }
+    }
+  }
+}
+
+__global__ void k_init_stats(uint32_t* st, uint32_t n) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) {
+    const uint32_t c = k % 5;
+    st[k] = (c == 1 || c == 2) ? 0xFFFFFFFFu : 0u;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_keypoints: projection + depth-tested visibility
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void project_one(const float* pv, const float* p, float Wf, float Hf, float nearc,
+                                            float& u, float& v, int& vis, int& px, int& py) {
+  const float X = dot4(pv + 0, p[0], p[1], p[2]);
+  const float Y = dot4(pv + 4, p[0], p[1], p[2]);
+  const float Wc = dot4(pv + 8, p[0], p[1], p[2]);
+  px = py = -1;
+  if (!(Wc >= nearc)) {
+    u = -1.0f; v = -1.0f; vis = 0;
+    return;
+  }
+  u = X / Wc;
+  v = Y / Wc;
+  if (!(u >= 0.0f && u < Wf && v >= 0.0f && v < Hf)) { vis = 0; return; }
+  px = (int)u;
+  py = (int)v;
+  vis = 1;
+}
+
+__global__ __launch_bounds__(256) void k_keypoints(SceneDev s, BatchDev b) {
+  const uint32_t f = blockIdx.y;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.n_kp) return;
+  const float* pv = b.pv + (size_t)f * 12;
+  const float* p = b.kp + ((size_t)b.frames[f].xform_set * b.n_kp + k) * 3;
+  float u, v;
+  int vis, px, py;
+  project_one(pv, p, (float)s.W, (float)s.H, s.near_clip, u, v, vis, px, py);
+  if (vis) {
+    const float Wc = dot4(pv + 8, p[0], p[1], p[2]);
+    const float d = b.depth[(size_t)f * s.W * s.H + (size_t)py * s.W + px];
+    vis = (Wc <= d) ? 2 : 1;
+  }
+  b.kp_uv[((size_t)f * b.n_kp + k) * 2 + 0] = u;
+  b.kp_uv[((size_t)f * b.n_kp + k) * 2 + 1] = v;
+  b.kp_vis[(size_t)f * b.n_kp + k] = vis;
+}
+
+__global__ void k_project(const float* pts, uint32_t n, const float* pv, float Wf, float Hf, float nearc, float* uv,
+                          int32_t* vis) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  float u, v;
+  int vs, px, py;
+  project_one(pv, pts + (size_t)k * 3, Wf, Hf, nearc, u, v, vs, px, py);
+  uv[2 * k] = u;
+  uv[2 * k + 1] = v;
+  vis[k] = vs;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+  dim3 g((s.n_inst + 255) / 256, F);
+  hipLaunchKernelGGL(k_clip, g, dim3(256), 0, st, s, b);
+}
+
+void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks, uint32_t F,
+                  hipStream_t st) {
+  dim3 g(n_chunks, F);
+  hipLaunchKernelGGL(k_setup, g, dim3(kBlock), s.n_tiles * sizeof(uint32_t), st, s, b, chunks);
+}
+
+void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+  hipLaunchKernelGGL(k_scan, dim3(F), dim3(kBlock), 0, st, s, b);
+}
+
+void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+  dim3 g(64, F);
+  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), 2 * s.n_tiles * sizeof(uint32_t), st, s, b);
+}
+
+void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+  dim3 g(s.n_tiles, F);
+  hipLaunchKernelGGL(k_raster, g, dim3(kBlock), 0, st, s, b);
+}
+
+void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st) {
+  const uint32_t n = F * b.n_labels * 5;
+  if (!n || !b.stats) return;
+  hipLaunchKernelGGL(k_init_stats, dim3((n + 255) / 256), dim3(256), 0, st, b.stats, n);
+}
+
+void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+  if (!b.n_kp) return;
+  dim3 g((b.n_kp + 255) / 256, F);
+  hipLaunchKernelGGL(k_keypoints, g, dim3(256), 0, st, s, b);
+}
+
+void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip, float* uv,
+                    int32_t* vis, hipStream_t st) {
+  hipLaunchKernelGGL(k_project, dim3((n + 255) / 256), dim3(256), 0, st, pts, n, pv12, W, H, near_clip, uv, vis);
+}
+
+}  // namespace csg

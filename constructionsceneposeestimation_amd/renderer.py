@@ -1,0 +1,205 @@
+"""Python front-end of the C-ABI: one :class:`Renderer` per GPU per process.
+
+This is the object the reference's Camera + annotator graph collapses into:
+``Camera(...)`` + ``camera.initialize()`` (generate_construction_data.py:1421,
+:1451) become :class:`Renderer` construction, and each
+``set_world_pose`` + ``next_update_async`` + ``get_rgba()`` / ``get_data()``
+round trip (:1586-1595, :1669, :1681, :1916) becomes one row of a batched
+:meth:`Renderer.render` call.  Everything numeric runs in libcsg.so on the
+GPU; this module only marshals arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import CsgError
+from .camera_math import Intrinsics
+from .packing import PackedScene, light_constants, pack_scene
+from .scene.model import Scene
+
+FRAME_DTYPE = np.dtype([("view", "<f4", 16), ("proj", "<f4", 16), ("xform_set", "<u4"), ("frame_id", "<u4")])
+assert FRAME_DTYPE.itemsize == C.sizeof(_lib.Frame)
+
+OUTPUT_KINDS = ("rgb", "instance", "depth", "keypoints", "stats")
+
+
+def make_frames(views: np.ndarray, projs: np.ndarray, sets: Sequence[int], frame_ids: Sequence[int]) -> np.ndarray:
+    n = len(frame_ids)
+    fr = np.zeros(n, FRAME_DTYPE)
+    fr["view"] = np.asarray(views, np.float64).reshape(n, 16).astype(np.float32)
+    fr["proj"] = np.asarray(projs, np.float64).reshape(n, 16).astype(np.float32)
+    fr["xform_set"] = np.asarray(sets, np.uint32)
+    fr["frame_id"] = np.asarray(frame_ids, np.uint32)
+    return fr
+
+
+class Renderer:
+    def __init__(self, scene: Scene, width: int, height: int, max_frames: int = 8, device: int = 0,
+                 intrinsics: Optional[Intrinsics] = None, records_per_frame: int = 0, bins_per_frame: int = 0):
+        self.lib = _lib.load()
+        self.scene = scene
+        self.width, self.height = int(width), int(height)
+        self.max_frames = int(max_frames)
+        self.intr = intrinsics or Intrinsics(self.width, self.height)
+        cfg = _lib.Config(device, self.width, self.height, self.max_frames, self.intr.near, self.intr.far,
+                          records_per_frame, bins_per_frame)
+        ctx = C.c_void_p()
+        rc = self.lib.csg_create(C.byref(cfg), C.byref(ctx))
+        if rc != 0:
+            raise CsgError(f"csg_create failed ({rc})")
+        self.ctx = ctx
+        self.packed: PackedScene = pack_scene(scene)
+        self.n_inst = len(scene.instances)
+        self.n_labels = max(self.packed.n_labels, 1)
+        self.n_kp = 0
+        self._upload()
+
+    # -- lifecycle ------------------------------------------------------------
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            msg = self.lib.csg_last_error(self.ctx).decode(errors="replace")
+            raise CsgError(f"{what}: status {rc}: {msg}")
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.csg_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- scene ---------------------------------------------------------------
+    def _upload(self) -> None:
+        p = self.packed
+        keep = []
+        meshes = (_lib.Mesh * len(self.scene.meshes))()
+        for k, m in enumerate(self.scene.meshes):
+            pos = np.ascontiguousarray(m.positions, np.float32)
+            idx = np.ascontiguousarray(m.tris, np.uint32)
+            keep += [pos, idx]
+            has_uv = m.uvs.shape[0] > 0 and m.uv_tris.shape[0] == m.n_tris
+            meshes[k].positions = pos.ctypes.data
+            meshes[k].n_vertices = pos.shape[0]
+            meshes[k].indices = idx.ctypes.data
+            meshes[k].n_tris = idx.shape[0]
+            if has_uv:
+                uv = np.ascontiguousarray(m.uvs, np.float32)
+                uvi = np.ascontiguousarray(m.uv_tris, np.uint32)
+                keep += [uv, uvi]
+                meshes[k].uvs, meshes[k].n_uvs, meshes[k].uv_indices = uv.ctypes.data, uv.shape[0], uvi.ctypes.data
+            meshes[k].material = m.material
+        mats = (_lib.Material * len(p.materials))()
+        for k in range(len(p.materials)):
+            mats[k].base_color[:] = [int(x) for x in p.materials[k]["base"]]
+            mats[k].texture = int(p.materials[k]["texture"])
+            mats[k].alpha_test = int(p.materials[k]["alpha_test"])
+            mats[k].alpha_threshold = int(p.materials[k]["alpha_threshold"])
+        inst = (_lib.Instance * self.n_inst)()
+        for k in range(self.n_inst):
+            inst[k].model[:] = [float(x) for x in p.inst_model[k]]
+            inst[k].mesh = int(p.inst_mesh[k])
+            inst[k].inst_idx = int(p.inst_label[k])
+        self._check(self.lib.csg_upload_scene(self.ctx, meshes, len(self.scene.meshes), mats, len(p.materials), inst,
+                                              self.n_inst), "upload_scene")
+        for k, t in enumerate(self.scene.textures):
+            a = np.ascontiguousarray(t.rgba, np.uint8)
+            self._check(self.lib.csg_upload_texture(self.ctx, k, a.ctypes.data, a.shape[1], a.shape[0]),
+                        "upload_texture")
+        amb, sun, d, sky = light_constants(self.scene.light)
+        L = _lib.Light()
+        L.ambient[:] = [float(x) for x in amb]
+        L.sun[:] = [float(x) for x in sun]
+        L.sun_dir[:] = [float(x) for x in d]
+        L.sky[:] = [int(x) for x in sky]
+        self._check(self.lib.csg_set_light(self.ctx, C.byref(L)), "set_light")
+
+    def set_instance_transforms(self, set_id: int, models: np.ndarray) -> None:
+        m = np.ascontiguousarray(np.asarray(models, np.float64).reshape(-1, 16).astype(np.float32))
+        self._check(self.lib.csg_set_instance_transforms(self.ctx, set_id, m.ctypes.data, m.shape[0]),
+                    "set_instance_transforms")
+
+    def set_keypoints(self, set_id: int, pts_world: np.ndarray) -> None:
+        p = np.ascontiguousarray(np.asarray(pts_world, np.float64).reshape(-1, 3).astype(np.float32))
+        self._check(self.lib.csg_set_keypoints(self.ctx, set_id, p.ctypes.data, p.shape[0]), "set_keypoints")
+        self.n_kp = p.shape[0]
+
+    # -- rendering ------------------------------------------------------------
+    def render(self, frames: np.ndarray, want: Iterable[str] = ("rgb", "instance", "depth")) -> Dict[str, np.ndarray]:
+        """Render a batch to host numpy arrays (synchronous; includes D2H copies)."""
+        want = set(want)
+        frames = np.ascontiguousarray(frames, FRAME_DTYPE)
+        n = frames.shape[0]
+        H, W = self.height, self.width
+        out: Dict[str, np.ndarray] = {}
+        o = _lib.Outputs()
+        if "rgb" in want:
+            out["rgb"] = np.empty((n, H, W, 3), np.uint8)
+            o.rgb = out["rgb"].ctypes.data
+        if "instance" in want:
+            out["instance"] = np.empty((n, H, W), np.int32)
+            o.instance = out["instance"].ctypes.data
+        if "depth" in want:
+            out["depth"] = np.empty((n, H, W), np.float32)
+            o.depth = out["depth"].ctypes.data
+        if "keypoints" in want and self.n_kp:
+            out["keypoints_uv"] = np.empty((n, self.n_kp, 2), np.float32)
+            out["keypoints_vis"] = np.empty((n, self.n_kp), np.int32)
+            o.keypoints_uv = out["keypoints_uv"].ctypes.data
+            o.keypoints_vis = out["keypoints_vis"].ctypes.data
+        if "stats" in want:
+            out["inst_stats"] = np.empty((n, self.n_labels, 5), np.uint32)
+            o.inst_stats = out["inst_stats"].ctypes.data
+        o.n_labels = self.n_labels
+        o.on_device = 0
+        for s in range(0, n, self.max_frames):
+            e = min(n, s + self.max_frames)
+            oo = _lib.Outputs()
+            for name, arr, per in (("rgb", out.get("rgb"), None), ("instance", out.get("instance"), None),
+                                   ("depth", out.get("depth"), None), ("keypoints_uv", out.get("keypoints_uv"), None),
+                                   ("keypoints_vis", out.get("keypoints_vis"), None),
+                                   ("inst_stats", out.get("inst_stats"), None)):
+                if arr is not None:
+                    setattr(oo, name, arr[s:e].ctypes.data)
+            oo.n_labels, oo.on_device = o.n_labels, 0
+            self._check(self.lib.csg_render_batch(self.ctx, frames[s:e].ctypes.data, e - s, C.byref(oo)),
+                        "render_batch")
+        return out
+
+    def render_into(self, frames_ptr: int, n: int, frames_on_device: bool, rgb: int = 0, instance: int = 0,
+                    depth: int = 0, kp_uv: int = 0, kp_vis: int = 0, stats: int = 0, stream: int = 0) -> None:
+        """Enqueue a batch writing device buffers (raw pointers, e.g. torch ``data_ptr()``)."""
+        o = _lib.Outputs(rgb or None, instance or None, depth or None, kp_uv or None, kp_vis or None,
+                         stats or None, self.n_labels, 1)
+        self._check(self.lib.csg_render_batch_async(self.ctx, frames_ptr, n, int(frames_on_device), C.byref(o),
+                                                    stream or None), "render_batch_async")
+
+    def synchronize(self) -> None:
+        self._check(self.lib.csg_synchronize(self.ctx), "synchronize")
+
+    def batch_stats(self) -> Dict[str, float]:
+        st = _lib.BatchStats()
+        self._check(self.lib.csg_get_batch_stats(self.ctx, C.byref(st)), "get_batch_stats")
+        return {n: getattr(st, n) for n, _ in _lib.BatchStats._fields_}
+
+    def project_keypoints(self, pts_world: np.ndarray, view: np.ndarray, proj: np.ndarray):
+        p = np.ascontiguousarray(np.asarray(pts_world).reshape(-1, 3), np.float32)
+        v = np.ascontiguousarray(np.asarray(view).reshape(16), np.float32)
+        pr = np.ascontiguousarray(np.asarray(proj).reshape(16), np.float32)
+        uv = np.empty((p.shape[0], 2), np.float32)
+        vis = np.empty(p.shape[0], np.int32)
+        self._check(self.lib.csg_project_keypoints(self.ctx, p.ctypes.data, p.shape[0], v.ctypes.data, pr.ctypes.data,
+                                                   uv.ctypes.data, vis.ctypes.data), "project_keypoints")
+        return uv, vis

@@ -1,0 +1,153 @@
+/*
+ * csg_api.h — C ABI of the MI355X construction-scene frame generator
+ * (libcsg.so, built for gfx950).  Plain C99: no C++ or torch types cross
+ * this boundary.  Every entry point returns 0 on success, a negative
+ * csg_status on failure; csg_last_error() gives the message.
+ *
+ * What each entry point replaces in the reference
+ * (xander683/ConstructionScenePoseEstimation, generate_construction_data.py):
+ *
+ *   csg_create ................ Camera(prim_path, resolution) + clip/focal/aperture
+ *                               setup + camera.initialize()           :1421-1453
+ *   csg_upload_scene .......... the USD stage the RTX renderer reads  :1370
+ *   csg_upload_texture ........ material texture binding (OmniPBR
+ *                               diffuse/opacity maps)                 world2 materials
+ *   csg_set_light ............. setup_scene_lighting (dome 500,
+ *                               distant light clamped to 1500)        :1289-1345
+ *   csg_set_instance_transforms randomize_object_positions' xformOp
+ *                               edits (every 10 frames)               :914-1231, :1542
+ *   csg_set_keypoints ......... (new) 3D points whose 2D projection is
+ *                               annotated; the reference produces none
+ *   csg_render_batch .......... camera.set_world_pose + next_update_async
+ *                               + get_rgba / distance_to_image_plane /
+ *                               instance_segmentation .get_data()     :1586-1595, :1669,
+ *                                                                     :1681, :1475/:1909
+ *   csg_project_keypoints ..... 3D->2D projection with the frame's
+ *                               intrinsics (pinhole of :646-649)
+ *   csg_last_error / csg_destroy
+ *
+ * Threading: one context per device per process; a context is not
+ * thread-safe.  No global state.
+ */
+#ifndef CSG_API_H
+#define CSG_API_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CSG_ABI_VERSION 1
+
+typedef enum {
+  CSG_OK = 0,
+  CSG_ERR_INVALID = -1,      /* bad argument / state */
+  CSG_ERR_DEVICE = -2,       /* HIP runtime error */
+  CSG_ERR_OOM = -3,          /* device allocation failed */
+  CSG_ERR_OVERFLOW = -4,     /* a per-frame work buffer overflowed; raise caps */
+  CSG_ERR_LIMIT = -5         /* scene exceeds a fixed limit (instances, tris/mesh) */
+} csg_status;
+
+typedef struct csg_ctx csg_ctx;
+
+typedef struct {
+  int32_t device;            /* HIP device ordinal (after HIP_VISIBLE_DEVICES) */
+  uint32_t width, height;    /* output resolution, e.g. 1920x1080 */
+  uint32_t max_frames;       /* frames per csg_render_batch call (work buffers sized for it) */
+  float near_clip, far_clip; /* 0.5 / 250 m, generate_construction_data.py:1437 */
+  uint32_t records_per_frame;/* raster-triangle capacity per frame (0 = auto) */
+  uint32_t bins_per_frame;   /* tile-bin entry capacity per frame (0 = auto) */
+} csg_config;
+
+typedef struct {
+  const float* positions;    /* [n_vertices][3] object space */
+  uint32_t n_vertices;
+  const uint32_t* indices;   /* [n_tris][3] */
+  uint32_t n_tris;           /* < 2^20 */
+  const float* uvs;          /* [n_uvs][2] USD st, or NULL */
+  uint32_t n_uvs;
+  const uint32_t* uv_indices;/* [n_tris][3] into uvs, or NULL */
+  uint32_t material;
+} csg_mesh;
+
+typedef struct {
+  uint8_t base_color[4];     /* sRGB u8 albedo multiplier (alpha unused) */
+  int32_t texture;           /* texture id or -1 */
+  uint32_t alpha_test;       /* 1: discard fragments with texture alpha <= threshold */
+  uint32_t alpha_threshold;
+} csg_material;
+
+typedef struct {
+  float model[16];           /* row-major 4x4, column-vector convention p' = M p */
+  uint32_t mesh;
+  int32_t inst_idx;          /* value written to the instance mask; -1 = background */
+  uint32_t reserved[2];
+} csg_instance;
+
+typedef struct {
+  float ambient[3];          /* dome light contribution per channel */
+  float sun[3];              /* distant light contribution per channel */
+  float sun_dir[3];          /* unit vector toward the sun, world space */
+  uint8_t sky[4];            /* background RGB */
+} csg_light;
+
+typedef struct {
+  float view[16];            /* row-major world->camera (USD camera: -Z forward) */
+  float proj[16];            /* row-major; rows 0,1,3 give (u*w, v*w, w) in pixels */
+  uint32_t xform_set;        /* instance-transform set (randomisation epoch) */
+  uint32_t frame_id;
+} csg_frame;
+
+typedef struct {
+  /* Caller-owned buffers, [n_frames] leading dimension.  Any may be NULL. */
+  uint8_t* rgb;              /* [n][H][W][3] */
+  int32_t* instance;         /* [n][H][W], -1 background */
+  float* depth;              /* [n][H][W] distance to image plane, +inf no hit */
+  float* keypoints_uv;       /* [n][K][2] pixels */
+  int32_t* keypoints_vis;    /* [n][K] 0 out/behind, 1 occluded, 2 visible */
+  uint32_t* inst_stats;      /* [n][n_labels][5] = pixels, minx, miny, maxx, maxy */
+  uint32_t n_labels;
+  int32_t on_device;         /* 1: device pointers (stay in HBM), 0: host pointers */
+} csg_outputs;
+
+typedef struct {
+  uint64_t records;          /* raster triangles emitted (all frames of the last batch) */
+  uint64_t bin_entries;      /* tile-bin entries */
+  float ms_setup, ms_bin, ms_raster, ms_keypoints, ms_total;   /* HIP-event timings */
+} csg_batch_stats;
+
+int csg_create(const csg_config* cfg, csg_ctx** out);
+void csg_destroy(csg_ctx* ctx);
+const char* csg_last_error(const csg_ctx* ctx);
+int csg_abi_version(void);
+
+int csg_upload_scene(csg_ctx* ctx, const csg_mesh* meshes, uint32_t n_meshes,
+                     const csg_material* materials, uint32_t n_materials,
+                     const csg_instance* instances, uint32_t n_instances);
+int csg_upload_texture(csg_ctx* ctx, uint32_t tex_id, const uint8_t* rgba8, uint32_t width,
+                       uint32_t height);
+int csg_set_light(csg_ctx* ctx, const csg_light* light);
+/* n must equal the scene's instance count; set_id < 4096. */
+int csg_set_instance_transforms(csg_ctx* ctx, uint32_t set_id, const float* model4x4, uint32_t n);
+/* World-space keypoints of one transform set: [n][3]; n is fixed per scene. */
+int csg_set_keypoints(csg_ctx* ctx, uint32_t set_id, const float* pts_world, uint32_t n);
+
+/* Render n_frames (<= max_frames) frames; synchronous. */
+int csg_render_batch(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out);
+/* Same, enqueued on `stream` (a hipStream_t, NULL = context stream); frames
+ * may be a device pointer when frames_on_device = 1.  Returns after enqueue. */
+int csg_render_batch_async(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames,
+                           int32_t frames_on_device, const csg_outputs* out, void* stream);
+int csg_synchronize(csg_ctx* ctx);
+int csg_get_batch_stats(csg_ctx* ctx, csg_batch_stats* st);
+
+/* Stand-alone 3D->2D projection (host buffers): uv [n][2], vis [n] without a
+ * depth test (1 = in front and inside the image, 0 otherwise). */
+int csg_project_keypoints(csg_ctx* ctx, const float* pts_world, uint32_t n, const float* view,
+                          const float* proj, float* uv_out, int32_t* vis_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CSG_API_H */

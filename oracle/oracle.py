@@ -1,0 +1,165 @@
+"""ctypes front-end of the CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+Loaded by tests/, ``__graft_entry__.smoke()`` and bench.py's cpu_baseline
+leg, as the checker.  The product path (``constructionsceneposeestimation_amd``)
+never imports this module.  Render parity against the reference's RTX
+renderer is unpinned (closed, absent); see csg_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+
+
+class _Scene(C.Structure):
+    _fields_ = [
+        ("positions", C.c_void_p), ("tris", C.c_void_p), ("uvs", C.c_void_p), ("uv_tris", C.c_void_p),
+        ("meshes", C.c_void_p), ("n_meshes", C.c_uint32),
+        ("inst_model", C.c_void_p), ("inst_mesh", C.c_void_p), ("inst_label", C.c_void_p),
+        ("inst_tri_base", C.c_void_p), ("n_inst", C.c_uint32),
+        ("materials", C.c_void_p), ("n_materials", C.c_uint32),
+        ("texels", C.c_void_p), ("textures", C.c_void_p), ("n_textures", C.c_uint32),
+        ("ambient", C.c_float * 3), ("sun", C.c_float * 3), ("sun_dir", C.c_float * 3),
+        ("sky", C.c_uint8 * 4),
+        ("width", C.c_uint32), ("height", C.c_uint32),
+        ("near_clip", C.c_float), ("far_clip", C.c_float),
+    ]
+
+
+class _Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("n_tris_in", "n_culled", "n_clipped", "n_raster_tris",
+                                           "n_fragments", "n_alpha_killed")]
+
+
+def build() -> str:
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < max(
+            os.path.getmtime(os.path.join(_HERE, f)) for f in ("csg_oracle.c", "csg_oracle.h")):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build())
+        vp, u32 = C.c_void_p, C.c_uint32
+        _lib.oracle_render_frame.argtypes = [C.POINTER(_Scene), vp, vp, vp, vp, vp, vp, u32, C.POINTER(_Stats)]
+        _lib.oracle_keypoints.argtypes = [C.POINTER(_Scene), vp, vp, vp, u32, vp, vp, vp]
+        _lib.oracle_render_frames.argtypes = [C.POINTER(_Scene), vp, vp, u32, vp, vp, vp, C.c_int]
+        _lib.oracle_mat4_mul.argtypes = [vp, vp, vp]
+    return _lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+class Oracle:
+    """Holds a packed scene (see ``packing.PackedScene``) and renders frames."""
+
+    def __init__(self, packed, width: int, height: int, near: float = 0.5, far: float = 250.0):
+        self.p = packed
+        self.width, self.height = width, height
+        self._keep = []
+        s = _Scene()
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(a, dt)
+            self._keep.append(a)
+            return a.ctypes.data
+
+        s.positions = arr(packed.positions, np.float32)
+        s.tris = arr(packed.tris, np.uint32)
+        s.uvs = arr(packed.uvs, np.float32)
+        s.uv_tris = arr(packed.uv_tris, np.uint32)
+        s.meshes = arr(packed.meshes, np.uint32)
+        s.n_meshes = packed.meshes.shape[0]
+        s.inst_model = arr(packed.inst_model, np.float32)
+        s.inst_mesh = arr(packed.inst_mesh, np.uint32)
+        s.inst_label = arr(packed.inst_label, np.int32)
+        s.inst_tri_base = arr(packed.inst_tri_base, np.uint32)
+        s.n_inst = packed.inst_mesh.shape[0]
+        mats = np.ascontiguousarray(packed.materials)
+        self._keep.append(mats)
+        s.materials = mats.ctypes.data
+        s.n_materials = mats.shape[0]
+        s.texels = arr(packed.texels, np.uint8)
+        texd = np.ascontiguousarray(packed.textures)
+        self._keep.append(texd)
+        s.textures = texd.ctypes.data
+        s.n_textures = texd.shape[0]
+        s.ambient[:] = [float(x) for x in packed.ambient]
+        s.sun[:] = [float(x) for x in packed.sun]
+        s.sun_dir[:] = [float(x) for x in packed.sun_dir]
+        s.sky[:] = [int(x) for x in packed.sky]
+        s.width, s.height = width, height
+        s.near_clip, s.far_clip = near, far
+        self.s = s
+
+    def set_instance_models(self, models16: np.ndarray) -> None:
+        a = np.ascontiguousarray(models16, np.float32).reshape(-1, 16)
+        assert a.shape[0] == self.s.n_inst
+        self._keep.append(a)
+        self.s.inst_model = a.ctypes.data
+
+    def render(self, view: np.ndarray, proj: np.ndarray, want_stats: bool = False):
+        H, W = self.height, self.width
+        rgb = np.empty((H, W, 3), np.uint8)
+        inst = np.empty((H, W), np.int32)
+        depth = np.empty((H, W), np.float32)
+        nl = max(int(self.p.n_labels), 1)
+        stats = np.empty((nl, 5), np.uint32)
+        st = _Stats()
+        v = np.ascontiguousarray(view, np.float32).reshape(16)
+        pr = np.ascontiguousarray(proj, np.float32).reshape(16)
+        rc = lib().oracle_render_frame(C.byref(self.s), _ptr(v), _ptr(pr), _ptr(rgb), _ptr(inst), _ptr(depth),
+                                       _ptr(stats), nl, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"oracle_render_frame failed: {rc}")
+        out = {"rgb": rgb, "instance": inst, "depth": depth, "inst_stats": stats}
+        if want_stats:
+            out["stats"] = {n: int(getattr(st, n)) for n, _ in _Stats._fields_}
+        return out
+
+    def keypoints(self, view, proj, pts: np.ndarray, depth: np.ndarray):
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+        uv = np.empty((pts.shape[0], 2), np.float32)
+        vis = np.empty(pts.shape[0], np.int32)
+        v = np.ascontiguousarray(view, np.float32).reshape(16)
+        pr = np.ascontiguousarray(proj, np.float32).reshape(16)
+        d = np.ascontiguousarray(depth, np.float32)
+        lib().oracle_keypoints(C.byref(self.s), _ptr(v), _ptr(pr), _ptr(pts), pts.shape[0], _ptr(d),
+                               _ptr(uv), _ptr(vis))
+        return uv, vis
+
+    def render_many(self, views: np.ndarray, projs: np.ndarray, threads: int = 1, outputs: bool = True):
+        n = views.shape[0]
+        H, W = self.height, self.width
+        rgb = np.empty((n, H, W, 3), np.uint8) if outputs else None
+        inst = np.empty((n, H, W), np.int32) if outputs else None
+        depth = np.empty((n, H, W), np.float32) if outputs else None
+        v = np.ascontiguousarray(views, np.float32).reshape(n, 16)
+        pr = np.ascontiguousarray(projs, np.float32).reshape(n, 16)
+        rc = lib().oracle_render_frames(C.byref(self.s), _ptr(v), _ptr(pr), n, _ptr(rgb), _ptr(inst),
+                                        _ptr(depth), threads)
+        if rc != 0:
+            raise RuntimeError("oracle_render_frames failed")
+        return rgb, inst, depth
+
+
+def mat4_mul_f32(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, np.float32).reshape(16)
+    b = np.ascontiguousarray(b, np.float32).reshape(16)
+    c = np.empty(16, np.float32)
+    lib().oracle_mat4_mul(_ptr(a), _ptr(b), _ptr(c))
+    return c.reshape(4, 4)

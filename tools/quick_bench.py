@@ -1,0 +1,55 @@
+"""Quick GPU timing probe: world2 at 1080p, batches of F frames, device outputs."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd.renderer import Renderer, make_frames
+    from constructionsceneposeestimation_amd.scene import load_world2
+
+    W, H = 1920, 1080
+    F = int(os.environ.get("F", "32"))
+    iters = int(os.environ.get("ITERS", "10"))
+    scene = load_world2()
+    intr = cm.Intrinsics(W, H)
+    rng = np.random.default_rng(0)
+    views, projs = [], []
+    for k in range(F):
+        cam = [rng.uniform(-10, 8), rng.uniform(-10, 10), [1.6, 1.7, 1.8, 2.0, 2.5, 3.0][k % 6]]
+        aim = [rng.uniform(-3, 3), rng.uniform(-3, 3), cam[2]]
+        V, P, _ = cm.frame_matrices(cam, cm.look_at_world_quat(cam, aim), intr)
+        views.append(V)
+        projs.append(P)
+    fr = make_frames(np.stack(views), np.stack(projs), [0] * F, list(range(F)))
+    r = Renderer(scene, W, H, max_frames=F)
+    dev = torch.device("cuda:0")
+    rgb = torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev)
+    inst = torch.empty((F, H, W), dtype=torch.int32, device=dev)
+    depth = torch.empty((F, H, W), dtype=torch.float32, device=dev)
+    frames_dev = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):
+        r.render_into(frames_dev.data_ptr(), F, True, rgb.data_ptr(), inst.data_ptr(), depth.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    print("warm stats", r.batch_stats(), flush=True)
+    t = time.perf_counter()
+    for _ in range(iters):
+        r.render_into(frames_dev.data_ptr(), F, True, rgb.data_ptr(), inst.data_ptr(), depth.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    st = r.batch_stats()
+    print(f"F={F} iters={iters}: {dt / iters * 1e3:.2f} ms/batch, {F * iters / dt:.1f} frames/s", flush=True)
+    print("stats", st, flush=True)
+    print("bg frac", float((inst < 0).float().mean()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
