@@ -16,7 +16,7 @@ EXPORTED = (
     "csg_create", "csg_destroy", "csg_last_error", "csg_abi_version", "csg_upload_scene",
     "csg_upload_texture", "csg_set_light", "csg_set_instance_transforms", "csg_set_keypoints",
     "csg_render_batch", "csg_render_batch_async", "csg_synchronize", "csg_get_batch_stats",
-    "csg_project_keypoints",
+    "csg_project_keypoints", "csg_timing_reset", "csg_timing_read",
 )
 
 
@@ -68,6 +68,11 @@ class BatchStats(C.Structure):
                 ("ms_total", C.c_float)]
 
 
+class Timing(C.Structure):
+    _fields_ = [("batches", C.c_uint32), ("frames", C.c_uint32), ("ms_setup", C.c_double),
+                ("ms_bin", C.c_double), ("ms_raster", C.c_double), ("ms_keypoints", C.c_double)]
+
+
 _lib: Optional[C.CDLL] = None
 
 
@@ -104,5 +109,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib.csg_synchronize.argtypes = [vp]
     lib.csg_get_batch_stats.argtypes = [vp, C.POINTER(BatchStats)]
     lib.csg_project_keypoints.argtypes = [vp, vp, u32, vp, vp, vp, vp]
+    lib.csg_timing_reset.argtypes = [vp]
+    lib.csg_timing_read.argtypes = [vp, C.POINTER(Timing)]
     _lib = lib
     return lib

@@ -101,9 +101,13 @@ struct csg_ctx {
   DevBuf<int32_t> o_kp_vis;
   DevBuf<uint32_t> o_stats;
 
-  // timing
+  // timing: ring of per-batch event quintuples (recorded, never waited on in the loop)
   bool timing = true;
-  hipEvent_t ev[6] = {};
+  static constexpr uint32_t kRing = 4096;
+  std::vector<hipEvent_t> ring;         // kRing * 5
+  std::vector<uint32_t> ring_frames;
+  uint64_t ring_count = 0;
+  hipEvent_t* ev = nullptr;             // events of the most recent batch
   uint32_t last_F = 0;
 
   int fail(int code, const char* fmt, ...) {
@@ -144,7 +148,10 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   c->n_tiles = c->tiles_x * c->tiles_y;
   hipError_t e = hipSetDevice(cfg->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  for (int k = 0; k < 6 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[k]);
+  c->ring.assign((size_t)csg_ctx::kRing * 5, nullptr);
+  c->ring_frames.assign(csg_ctx::kRing, 0);
+  for (size_t k = 0; k < c->ring.size() && e == hipSuccess; ++k) e = hipEventCreate(&c->ring[k]);
+  c->ev = c->ring.data();
   if (e != hipSuccess) {
     c->err = hipGetErrorString(e);
     csg_destroy(c);
@@ -164,7 +171,7 @@ void csg_destroy(csg_ctx* c) {
   c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
   if (c->h_frames) (void)hipHostFree(c->h_frames);
-  for (auto& e : c->ev)
+  for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -472,6 +479,12 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
   HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), st));
   launch_init_stats(b, F, st);
+  if (c->timing) {
+    const uint32_t slot = (uint32_t)(c->ring_count % csg_ctx::kRing);
+    c->ev = &c->ring[(size_t)slot * 5];
+    c->ring_frames[slot] = F;
+    ++c->ring_count;
+  }
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[0], st));
   launch_clip(s, b, F, st);
   launch_setup(s, b, c->chunks.p, c->n_chunks, F, st);
@@ -560,6 +573,35 @@ int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
     st->ms_keypoints = e;
     st->ms_total = a + b + d + e;
   }
+  return CSG_OK;
+}
+
+int csg_timing_reset(csg_ctx* c) {
+  if (!c) return CSG_ERR_INVALID;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->ring_count = 0;
+  return CSG_OK;
+}
+
+int csg_timing_read(csg_ctx* c, csg_timing* out) {
+  if (!c || !out) return CSG_ERR_INVALID;
+  memset(out, 0, sizeof(*out));
+  const uint64_t n = std::min<uint64_t>(c->ring_count, csg_ctx::kRing);
+  for (uint64_t k = 0; k < n; ++k) {
+    hipEvent_t* e = &c->ring[(size_t)k * 5];
+    HIP_TRY(c, hipEventSynchronize(e[4]));
+    float a = 0, b = 0, d = 0, f = 0;
+    HIP_TRY(c, hipEventElapsedTime(&a, e[0], e[1]));
+    HIP_TRY(c, hipEventElapsedTime(&b, e[1], e[2]));
+    HIP_TRY(c, hipEventElapsedTime(&d, e[2], e[3]));
+    HIP_TRY(c, hipEventElapsedTime(&f, e[3], e[4]));
+    out->ms_setup += a;
+    out->ms_bin += b;
+    out->ms_raster += d;
+    out->ms_keypoints += f;
+    out->frames += c->ring_frames[k];
+  }
+  out->batches = (uint32_t)n;
   return CSG_OK;
 }
 

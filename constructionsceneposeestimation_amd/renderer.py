@@ -194,6 +194,14 @@ class Renderer:
         self._check(self.lib.csg_get_batch_stats(self.ctx, C.byref(st)), "get_batch_stats")
         return {n: getattr(st, n) for n, _ in _lib.BatchStats._fields_}
 
+    def timing_reset(self) -> None:
+        self._check(self.lib.csg_timing_reset(self.ctx), "timing_reset")
+
+    def timing_read(self) -> Dict[str, float]:
+        t = _lib.Timing()
+        self._check(self.lib.csg_timing_read(self.ctx, C.byref(t)), "timing_read")
+        return {n: getattr(t, n) for n, _ in _lib.Timing._fields_}
+
     def project_keypoints(self, pts_world: np.ndarray, view: np.ndarray, proj: np.ndarray):
         p = np.ascontiguousarray(np.asarray(pts_world).reshape(-1, 3), np.float32)
         v = np.ascontiguousarray(np.asarray(view).reshape(16), np.float32)

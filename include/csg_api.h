@@ -142,6 +142,18 @@ int csg_render_batch_async(csg_ctx* ctx, const csg_frame* frames, uint32_t n_fra
 int csg_synchronize(csg_ctx* ctx);
 int csg_get_batch_stats(csg_ctx* ctx, csg_batch_stats* st);
 
+/* Per-stage device time accumulated with HIP events recorded on the launch
+ * stream for every batch since the last reset (no host sync inside the
+ * timed loop).  Stages: setup = k_clip+k_setup, bin = k_scan+k_bin,
+ * raster = k_raster (tile raster + resolve), keypoints = k_keypoints. */
+typedef struct {
+  uint32_t batches;          /* batches accumulated (capped at the ring size, 4096) */
+  uint32_t frames;           /* frames in those batches */
+  double ms_setup, ms_bin, ms_raster, ms_keypoints;
+} csg_timing;
+int csg_timing_reset(csg_ctx* ctx);
+int csg_timing_read(csg_ctx* ctx, csg_timing* out);
+
 /* Stand-alone 3D->2D projection (host buffers): uv [n][2], vis [n] without a
  * depth test (1 = in front and inside the image, 0 otherwise). */
 int csg_project_keypoints(csg_ctx* ctx, const float* pts_world, uint32_t n, const float* view,

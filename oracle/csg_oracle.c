@@ -410,12 +410,15 @@ int oracle_keypoints(const oracle_scene* s, const float* view, const float* proj
 }
 
 int oracle_render_frames(const oracle_scene* s, const float* views, const float* projs,
-                         uint32_t n_frames, uint8_t* rgb, int32_t* inst, float* depth, int threads) {
+                         uint32_t n_frames, const float* models, uint8_t* rgb, int32_t* inst, float* depth,
+                         int threads) {
   const size_t npx = (size_t)s->width * s->height;
   int rc = 0;
 #pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(| : rc)
   for (int f = 0; f < (int)n_frames; ++f) {
-    rc |= oracle_render_frame(s, views + (size_t)f * 16, projs + (size_t)f * 16,
+    oracle_scene sf = *s;
+    if (models) sf.inst_model = models + (size_t)f * s->n_inst * 16;
+    rc |= oracle_render_frame(&sf, views + (size_t)f * 16, projs + (size_t)f * 16,
                               rgb ? rgb + npx * 3 * f : NULL, inst ? inst + npx * f : NULL,
                               depth ? depth + npx * f : NULL, NULL, 0, NULL);
   }

@@ -82,10 +82,11 @@ int oracle_keypoints(const oracle_scene* s, const float* view, const float* proj
 /* fp32 4x4 product with the fixed summation order of the spec. */
 void oracle_mat4_mul(const float* a, const float* b, float* c);
 
-/* Render n_frames frames with `threads` OpenMP threads (cpu baseline). */
+/* Render n_frames frames with `threads` OpenMP threads (cpu baseline).
+ * models: optional per-frame instance transforms [n_frames][n_inst][16]. */
 int oracle_render_frames(const oracle_scene* s, const float* views, const float* projs,
-                         uint32_t n_frames, uint8_t* rgb, int32_t* inst, float* depth,
-                         int threads);
+                         uint32_t n_frames, const float* models, uint8_t* rgb, int32_t* inst,
+                         float* depth, int threads);
 
 #ifdef __cplusplus
 }

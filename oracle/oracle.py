@@ -55,7 +55,7 @@ def lib():
         vp, u32 = C.c_void_p, C.c_uint32
         _lib.oracle_render_frame.argtypes = [C.POINTER(_Scene), vp, vp, vp, vp, vp, vp, u32, C.POINTER(_Stats)]
         _lib.oracle_keypoints.argtypes = [C.POINTER(_Scene), vp, vp, vp, u32, vp, vp, vp]
-        _lib.oracle_render_frames.argtypes = [C.POINTER(_Scene), vp, vp, u32, vp, vp, vp, C.c_int]
+        _lib.oracle_render_frames.argtypes = [C.POINTER(_Scene), vp, vp, u32, vp, vp, vp, vp, C.c_int]
         _lib.oracle_mat4_mul.argtypes = [vp, vp, vp]
     return _lib
 
@@ -142,7 +142,9 @@ class Oracle:
                                _ptr(uv), _ptr(vis))
         return uv, vis
 
-    def render_many(self, views: np.ndarray, projs: np.ndarray, threads: int = 1, outputs: bool = True):
+    def render_many(self, views: np.ndarray, projs: np.ndarray, threads: int = 1, outputs: bool = True,
+                    models: Optional[np.ndarray] = None):
+        """Render frames in parallel; ``models`` = optional per-frame [n][I][16] instance transforms."""
         n = views.shape[0]
         H, W = self.height, self.width
         rgb = np.empty((n, H, W, 3), np.uint8) if outputs else None
@@ -150,7 +152,8 @@ class Oracle:
         depth = np.empty((n, H, W), np.float32) if outputs else None
         v = np.ascontiguousarray(views, np.float32).reshape(n, 16)
         pr = np.ascontiguousarray(projs, np.float32).reshape(n, 16)
-        rc = lib().oracle_render_frames(C.byref(self.s), _ptr(v), _ptr(pr), n, _ptr(rgb), _ptr(inst),
+        m = None if models is None else np.ascontiguousarray(models, np.float32).reshape(n, -1)
+        rc = lib().oracle_render_frames(C.byref(self.s), _ptr(v), _ptr(pr), n, _ptr(m), _ptr(rgb), _ptr(inst),
                                         _ptr(depth), threads)
         if rc != 0:
             raise RuntimeError("oracle_render_frames failed")
