@@ -1,0 +1,107 @@
+"""Per-frame labels: 3D boxes, poses, visibility, keypoints, label JSON.
+
+Reference anchors (generate_construction_data.py):
+* ``bounding_box_3d`` annotator records — fields [1..6] local min/max, [7]
+  4x4 row-major transform, read positionally at :562-564;
+* ``bboxDict_to_transform`` :553-584 (centre = T^T mean(corners), size =
+  |max-min| * column scales, euler 'xyz' degrees of the SVD-orthonormalised
+  rotation) — restated here;
+* label record :2056-2064 and ``save_label_json`` :608-613; the instance
+  mask file ``instance_mask_%06d.npy`` :2066-2069.
+
+This build adds ``keypoints_2d`` (per object: 8 box corners + centre, and
+17 COCO joints for humans) and ``bbox_2d`` / ``pixel_count`` from the GPU's
+per-instance statistics.  ``inst_idx`` is the scene-stable object index (the
+reference numbers visible objects in Replicator's order, unknowable offline).
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+from scipy.spatial.transform import Rotation
+
+from .identity import CONSTRUCTION_CLASS
+
+BBOX3D_DTYPE = np.dtype([("semanticId", "<u4"), ("x_min", "<f4"), ("y_min", "<f4"), ("z_min", "<f4"),
+                         ("x_max", "<f4"), ("y_max", "<f4"), ("z_max", "<f4"), ("transform", "<f4", (4, 4)),
+                         ("occlusionRatio", "<f4")])
+
+
+def bbox3d_records(scene, object_frames: Sequence[np.ndarray]) -> np.ndarray:
+    """Replicator-style bounding_box_3d data for every labelled object."""
+    rec = np.zeros(len(scene.objects), BBOX3D_DTYPE)
+    for j, o in enumerate(scene.objects):
+        lo, hi = o.local_bounds if o.local_bounds is not None else (np.zeros(3), np.zeros(3))
+        rec[j]["semanticId"] = o.class_id
+        rec[j]["x_min"], rec[j]["y_min"], rec[j]["z_min"] = lo
+        rec[j]["x_max"], rec[j]["y_max"], rec[j]["z_max"] = hi
+        rec[j]["transform"] = np.asarray(object_frames[j]).T       # USD row-vector convention
+        rec[j]["occlusionRatio"] = -1.0
+    return rec
+
+
+def bboxDict_to_transform(bbox) -> tuple:
+    """(center_world[3], size_world[3], euler_xyz_deg[3]) of one record (:553-584)."""
+    corner = np.array([[bbox[1], bbox[2], bbox[3]], [bbox[4], bbox[5], bbox[6]]], dtype=np.float64)
+    T = np.asarray(bbox[7], dtype=np.float64).reshape(4, 4).T
+    center = (T @ np.append(corner.mean(axis=0), 1.0))[:3]
+    rot = T[:3, :3]
+    U, _, Vt = np.linalg.svd(rot)
+    euler = Rotation.from_matrix(U @ Vt).as_euler("xyz", degrees=True)
+    scale = np.linalg.norm(rot, axis=0)
+    size = scale * np.abs(corner[1] - corner[0])
+    return center.tolist(), size.tolist(), euler.tolist()
+
+
+def object_poses(scene, object_frames) -> List[dict]:
+    """Pose entries of every object (cache per randomisation epoch)."""
+    recs = bbox3d_records(scene, object_frames)
+    out = []
+    for j, o in enumerate(scene.objects):
+        r = recs[j]
+        c, s, e = bboxDict_to_transform((r["semanticId"], r["x_min"], r["y_min"], r["z_min"], r["x_max"],
+                                         r["y_max"], r["z_max"], r["transform"], r["occlusionRatio"]))
+        out.append({"inst_idx": o.inst_idx, "class_id": o.class_id, "class_name": o.class_name,
+                    "center": c, "size": s, "rotation": e, "prim_path": o.prim_path})
+    return out
+
+
+def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dict, poses: List[dict],
+                 inst_stats: Optional[np.ndarray], kp_uv: Optional[np.ndarray], kp_vis: Optional[np.ndarray],
+                 kp_table: Optional[Sequence], height: int, width: int) -> dict:
+    """The label JSON of one frame (:2056-2064) for the objects visible in it."""
+    objs = []
+    kp_by_obj: Dict[int, list] = {}
+    if kp_uv is not None and kp_table is not None:
+        for k, (j, name) in enumerate(kp_table):
+            kp_by_obj.setdefault(j, []).append(
+                [name, float(kp_uv[k, 0]), float(kp_uv[k, 1]), int(kp_vis[k])])
+    for j, p in enumerate(poses):
+        if inst_stats is not None:
+            cnt = int(inst_stats[p["inst_idx"], 0]) if p["inst_idx"] < inst_stats.shape[0] else 0
+            if cnt == 0:
+                continue
+        e = dict(p)
+        if inst_stats is not None:
+            st = inst_stats[p["inst_idx"]]
+            e["pixel_count"] = int(st[0])
+            e["bbox_2d"] = [int(st[1]), int(st[2]), int(st[3]), int(st[4])]
+        if j in kp_by_obj:
+            e["keypoints_2d"] = kp_by_obj[j]
+        objs.append(e)
+    return {
+        "frame_id": int(frame_id),
+        "camera_pose": [float(x) for x in camera_pose],
+        "camera_params": camera_params,
+        "objects": objs,
+        "instance_mask_shape": [int(height), int(width)],
+        "num_objects": len(objs),
+        "class_mapping": dict(CONSTRUCTION_CLASS),
+    }
+
+
+def save_label_json(label: dict, filename: str) -> None:
+    with open(filename, "w", encoding="utf-8") as f:
+        json.dump(label, f, indent=2, ensure_ascii=False)

@@ -1,0 +1,72 @@
+"""The C-ABI library builds, loads and exports every symbol include/csg_api.h
+declares; ctypes struct layouts match the C compiler's (no GPU calls)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "csg_api.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(csg_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = declared_functions()
+    for f in ("csg_create", "csg_upload_scene", "csg_upload_texture", "csg_set_instance_transforms",
+              "csg_render_batch", "csg_project_keypoints", "csg_last_error", "csg_destroy"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from constructionsceneposeestimation_amd import _lib
+    lib = _lib.load()
+    for f in declared_functions():
+        assert hasattr(lib, f), f
+    assert set(declared_functions()) == set(_lib.EXPORTED)
+    assert lib.csg_abi_version() == 1
+
+
+def test_invalid_config_rejected_without_gpu():
+    """csg_create validates its arguments before touching HIP."""
+    from constructionsceneposeestimation_amd import _lib
+    lib = _lib.load()
+    ctx = C.c_void_p()
+    bad = _lib.Config(0, 0, 1080, 8, 0.5, 250.0, 0, 0)
+    assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
+    bad = _lib.Config(0, 1920, 1080, 8, 0.5, 0.1, 0, 0)
+    assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
+
+
+def test_struct_layouts_match_c():
+    from constructionsceneposeestimation_amd import _lib
+    names = {"csg_config": _lib.Config, "csg_mesh": _lib.Mesh, "csg_material": _lib.Material,
+             "csg_instance": _lib.Instance, "csg_light": _lib.Light, "csg_frame": _lib.Frame,
+             "csg_outputs": _lib.Outputs, "csg_batch_stats": _lib.BatchStats, "csg_timing": _lib.Timing}
+    prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"csg_api.h\"\nint main(){\n"
+    for n in names:
+        prog += f'printf("{n} %zu\\n", sizeof({n}));\n'
+    prog += "return 0;}\n"
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "t")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
+    sizes = dict(line.split() for line in out.strip().splitlines())
+    for n, cls in names.items():
+        assert int(sizes[n]) == C.sizeof(cls), n
+
+
+def test_frame_dtype_matches_abi():
+    import numpy as np
+    from constructionsceneposeestimation_amd import _lib
+    from constructionsceneposeestimation_amd.renderer import FRAME_DTYPE
+    assert FRAME_DTYPE.itemsize == C.sizeof(_lib.Frame) == 136
