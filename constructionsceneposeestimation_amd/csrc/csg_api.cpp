@@ -7,6 +7,7 @@
 // on the host, before anything is uploaded.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -109,6 +110,8 @@ struct csg_ctx {
   uint64_t ring_count = 0;
   hipEvent_t* ev = nullptr;             // events of the most recent batch
   uint32_t last_F = 0;
+  uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
+  int raster_variant = 0;               // k_raster expansion variant (CSG_VARIANT overrides; A/B only)
 
   int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -143,6 +146,8 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
     return CSG_ERR_INVALID;
   csg_ctx* c = new csg_ctx();
   c->cfg = *cfg;
+  if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
+  if (const char* v = getenv("CSG_VARIANT")) c->raster_variant = atoi(v);
   c->tiles_x = (cfg->width + kTile - 1) / kTile;
   c->tiles_y = (cfg->height + kTile - 1) / kTile;
   c->n_tiles = c->tiles_x * c->tiles_y;
@@ -229,7 +234,20 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
     ilabel[i] = inst[i].inst_idx;
     memcpy(&models[(size_t)i * 16], inst[i].model, 16 * sizeof(float));
     const uint32_t nt = md[inst[i].mesh].ntris;
-    for (uint32_t s0 = 0; s0 < nt; s0 += kBlock) ch.push_back(Chunk{i, s0, std::min<uint32_t>(kBlock, nt - s0), 0});
+    const MeshDesc& md_i = md[inst[i].mesh];
+    for (uint32_t s0 = 0; s0 < nt; s0 += kBlock) {
+      Chunk c0{};
+      c0.inst = i;
+      c0.start = s0;
+      c0.count = std::min<uint32_t>(kBlock, nt - s0);
+      for (int a = 0; a < 3; ++a) { c0.lo[a] = INFINITY; c0.hi[a] = -INFINITY; }
+      for (uint32_t t = s0; t < s0 + c0.count; ++t)
+        for (int k = 0; k < 3; ++k) {
+          const float* p = &pos[((size_t)md_i.vbase + tris[((size_t)md_i.tbase + t) * 3 + k]) * 3];
+          for (int a = 0; a < 3; ++a) { c0.lo[a] = std::min(c0.lo[a], p[a]); c0.hi[a] = std::max(c0.hi[a], p[a]); }
+        }
+      ch.push_back(c0);
+    }
     ntot += nt;
   }
   if (ch.empty()) return c->fail(CSG_ERR_INVALID, "upload_scene: no triangles");
@@ -379,7 +397,7 @@ static int ensure_work(csg_ctx* c, uint32_t F) {
   HIP_TRY(c, c->pv.alloc((size_t)maxF * 12));
   HIP_TRY(c, c->recs.alloc((size_t)maxF * c->rec_cap));
   HIP_TRY(c, c->rect.alloc((size_t)maxF * c->rec_cap));
-  HIP_TRY(c, c->rec_count.alloc(maxF));
+  HIP_TRY(c, c->rec_count.alloc((size_t)maxF * kCounterStride));
   HIP_TRY(c, c->tile_count.alloc((size_t)maxF * c->n_tiles));
   HIP_TRY(c, c->tile_off.alloc((size_t)maxF * (c->n_tiles + 1)));
   HIP_TRY(c, c->tile_fill.alloc((size_t)maxF * c->n_tiles));
@@ -449,6 +467,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   b.bin_cap = c->bin_cap;
   b.overflow = c->overflow.p;
   b.n_labels = out->n_labels;
+  b.dbg = c->dbg;
   b.kp = c->kp.p;
   b.n_kp = want_kp ? c->n_kp : 0;
   if (dev) {
@@ -474,7 +493,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (!b.kp_vis) { HIP_TRY(c, c->o_kp_vis.alloc((size_t)F * c->n_kp)); b.kp_vis = c->o_kp_vis.p; }
   }
   SceneDev s = scene_dev(c);
-  HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * F, st));
+  HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * F * kCounterStride, st));
   HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
   HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
   HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), st));
@@ -489,10 +508,11 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   launch_clip(s, b, F, st);
   launch_setup(s, b, c->chunks.p, c->n_chunks, F, st);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
+  launch_count(s, b, F, st);
   launch_scan(s, b, F, st);
   launch_bin(s, b, F, st);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
-  launch_raster(s, b, F, st);
+  launch_raster(s, b, F, st, c->raster_variant);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
   launch_keypoints(s, b, F, st);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
@@ -554,8 +574,9 @@ int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   const uint32_t F = c->last_F;
   if (!F) return CSG_OK;
-  std::vector<uint32_t> rc(F), to((size_t)F * (c->n_tiles + 1));
-  HIP_TRY(c, hipMemcpy(rc.data(), c->rec_count.p, F * 4, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> rcs((size_t)F * kCounterStride), rc(F), to((size_t)F * (c->n_tiles + 1));
+  HIP_TRY(c, hipMemcpy(rcs.data(), c->rec_count.p, rcs.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t f = 0; f < F; ++f) rc[f] = rcs[(size_t)f * kCounterStride];
   HIP_TRY(c, hipMemcpy(to.data(), c->tile_off.p, to.size() * 4, hipMemcpyDeviceToHost));
   for (uint32_t f = 0; f < F; ++f) {
     st->records += std::min(rc[f], c->rec_cap);

@@ -13,11 +13,17 @@ constexpr uint32_t kUidShift = 20;        // uid = (instance << 20) | triangle
 constexpr uint32_t kMaxInstances = 1u << (32 - kUidShift);
 constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
 constexpr int kMaxLdsLabels = 256;        // per-label pixel stats kept in LDS
+constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
 
 struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };
 struct MatDesc { uint8_t base[4]; int32_t texture; uint32_t alpha_test, alpha_threshold; };
 struct TexDesc { uint32_t offset, width, height, pad; };
-struct Chunk { uint32_t inst, start, count, pad; };   // <= 256 triangles of one instance
+struct Chunk {                    // <= 256 triangles of one instance + their object-space AABB
+  uint32_t inst, start, count, pad;
+  float lo[3], hi[3];
+  uint32_t pad2[2];
+};
+static_assert(sizeof(Chunk) == 48, "Chunk layout");
 
 // One raster (sub-)triangle: fixed-point screen vertices for coverage plus the
 // homogeneous coefficients of its ORIGINAL triangle for depth/attributes.
@@ -66,7 +72,7 @@ struct BatchDev {
   Rec* recs;                   // [F][rec_cap]
   uint32_t* rect;              // [F][rec_cap] tile rect tx0|ty0<<8|tx1<<16|ty1<<24
   uint32_t rec_cap;
-  uint32_t* rec_count;         // [F]
+  uint32_t* rec_count;         // [F * kCounterStride] (one cache line per frame: no atomic contention)
   uint32_t* tile_count;        // [F][n_tiles]
   uint32_t* tile_off;          // [F][n_tiles+1]
   uint32_t* tile_fill;         // [F][n_tiles]
@@ -83,15 +89,17 @@ struct BatchDev {
   uint32_t n_kp;
   float* kp_uv;                // [F][K][2]
   int32_t* kp_vis;             // [F][K]
+  uint32_t dbg;                // ablation switches for profiling only (CSG_DEBUG env; 0 in production)
 };
 
 // launchers (all enqueue on `st`)
 void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks,
                   uint32_t F, hipStream_t st);
+void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
-void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st, int variant);
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip,

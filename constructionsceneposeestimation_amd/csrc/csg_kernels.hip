@@ -10,9 +10,10 @@
 //
 // Pipeline per batch of F frames (all frames of a batch in every launch):
 //   k_clip     (F x instances)   P*V*M in fp32, fixed summation order
-//   k_setup    (chunks x F)      transform, cull, near-clip, fixed-point
-//                                setup, wave-ballot record append, LDS tile
-//                                histogram -> per-tile counts
+//   k_setup    (chunks x F)      chunk AABB cull, transform, triangle cull,
+//                                near-clip, fixed-point setup, wave-ballot
+//                                record append
+//   k_count    (64 x F)          LDS-aggregated per-tile record counts
 //   k_scan     (F)               exclusive scan of tile counts
 //   k_bin      (64 x F)          LDS-aggregated scatter of record ids to bins
 //   k_raster   (tiles x F)       32x32 tile: bins staged in LDS, balanced
@@ -22,6 +23,8 @@
 //                                depth, coalesced HBM writes, label stats
 //   k_keypoints(K x F)           3D->2D projection + depth-tested visibility
 #include <math.h>
+
+#include <type_traits>
 
 #include "csg_kernels.h"
 
@@ -146,6 +149,38 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   return off + inc - v;
 }
 
+// Order this wave's earlier LDS writes before its later LDS reads (cross-lane).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t n = __shfl_up(v, d, 64);
+    if (lane >= d) v = max(v, n);
+  }
+  return v;
+}
+
+// Owner lane of window item `lane` for ranges that start at window offset
+// `rel` (sorted by lane; `has` = the lane's range is non-empty).  `carry` is
+// the owner of the item just before the window and is updated in place.
+__device__ __forceinline__ uint32_t window_owner(uint32_t* mark, int lane, bool has, uint32_t rel, uint32_t& carry) {
+  mark[lane] = 0;
+  wave_lds_sync();
+  if (has && rel < 64u) mark[rel] = (uint32_t)lane + 1u;
+  wave_lds_sync();
+  const uint32_t m = wave_incl_max(mark[lane]);
+  const uint32_t own = m ? m - 1u : carry;
+  carry = __builtin_amdgcn_readlane(own, 63);
+  wave_lds_sync();
+  return own;
+}
+
 // last k in [0,256) with pre[k] <= j  (pre has 257 entries, j < pre[256])
 __device__ __forceinline__ int find_item(const uint32_t* pre, uint32_t j) {
   int lo = 0;
@@ -246,21 +281,41 @@ __device__ __forceinline__ uint32_t rect_tile(uint32_t rc, uint32_t q, uint32_t 
 }
 
 __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chunk* __restrict__ chunks) {
-  extern __shared__ uint32_t hist[];                 // [n_tiles]
-  __shared__ uint32_t big[2 * kBlock];
-  __shared__ uint32_t n_big;
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63;
+  if (b.dbg & 32u) return;            // ablation: empty setup
   const Chunk ch = chunks[blockIdx.x];
-  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
-  if (tid == 0) n_big = 0;
+  const uint32_t i = ch.inst;
+  const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
+  // Chunk cull: every wave evaluates the 8 corners of the chunk's object-space
+  // AABB (lanes 0-7) and the block leaves if all corners fail one frustum
+  // plane by a margin -- then every triangle inside would fail that plane in
+  // the per-triangle test too, so the output is unchanged.
+  {
+    bool out_n = true, out_f = true, out_l = true, out_r = true, out_t = true, out_b = true;
+    const int cidx = lane & 7;
+    const float px = (cidx & 4) ? ch.hi[0] : ch.lo[0];
+    const float py = (cidx & 2) ? ch.hi[1] : ch.lo[1];
+    const float pz = (cidx & 1) ? ch.hi[2] : ch.lo[2];
+    const float X = dot4(Cm + 0, px, py, pz), Y = dot4(Cm + 4, px, py, pz), Wc = dot4(Cm + 8, px, py, pz);
+    const float tol = 1e-3f * (fabsf(X) + fabsf(Y) + fabsf(Wc)) + 1e-3f;
+    out_n = Wc < s.near_clip - tol;
+    out_f = Wc > s.far_clip + tol;
+    out_l = X < -tol;
+    out_r = X > (float)s.W * Wc + tol * (float)s.W;
+    out_t = Y < -tol;
+    out_b = Y > (float)s.H * Wc + tol * (float)s.H;
+    const uint64_t m8 = 0xFFull;
+    const bool cull = ((__ballot(out_n) & m8) == m8) || ((__ballot(out_f) & m8) == m8) ||
+                      ((__ballot(out_l) & m8) == m8) || ((__ballot(out_r) & m8) == m8) ||
+                      ((__ballot(out_t) & m8) == m8) || ((__ballot(out_b) & m8) == m8);
+    if (cull || (b.dbg & 64u)) return;   // identical in every wave of the block (64: ablation, cull all)
+  }
 
   Rec r0, r1;   // named, never runtime-indexed (a Rec[2] would live in scratch)
   int nrec = 0;
-  const uint32_t i = ch.inst;
   if ((uint32_t)tid < ch.count) {
     const uint32_t t = ch.start + tid;
-    const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
     float c[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) c[k] = Cm[k];
@@ -366,34 +421,58 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   const uint32_t mine = (uint32_t)(__popcll(b1 & lt) + __popcll(b2 & lt));
   const uint32_t wtot = (uint32_t)(__popcll(b1) + __popcll(b2));
   uint32_t wbase = 0;
-  if (lane == 0 && wtot) wbase = atomicAdd(&b.rec_count[f], wtot);
+  if (lane == 0 && wtot) wbase = atomicAdd(&b.rec_count[f * kCounterStride], wtot);
   wbase = __shfl(wbase, 0, 64);
-  __syncthreads();   // hist zeroed
   auto emit = [&](const Rec& rec, uint32_t slot) {
     if (slot >= b.rec_cap) {
       atomicOr(b.overflow, 1u);
       return;
     }
     store_rec(b.recs + (size_t)f * b.rec_cap + slot, rec);
-    const uint32_t rc = rec_tile_rect(rec);
-    b.rect[(size_t)f * b.rec_cap + slot] = rc;
-    const uint32_t area = rect_area(rc);
-    if (area <= (uint32_t)kSmallRect) {
-      for (uint32_t q = 0; q < area; ++q) atomicAdd(&hist[rect_tile(rc, q, s.tiles_x)], 1u);
-    } else {
-      big[atomicAdd(&n_big, 1u)] = rc;
-    }
+    b.rect[(size_t)f * b.rec_cap + slot] = rec_tile_rect(rec);
   };
+  if (b.dbg & 128u) {   // ablation: no record stores
+    if (nrec == 3 && b.inst) b.inst[0] = r0.uid + r1.uid;
+    return;
+  }
   if (nrec > 0) emit(r0, wbase + mine);
   if (nrec > 1) emit(r1, wbase + mine + 1);
+}
+
+// ---------------------------------------------------------------------------
+// k_count: per-tile record counts (LDS-aggregated, grid-stride over a frame's records)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_count[];
+  uint32_t* hist = dyn_count;                          // [n_tiles]
+  uint32_t* pre = dyn_count + ((s.n_tiles + 3u) & ~3u);   // [kBlock + 1]
+  uint32_t* lrc = pre + kBlock + 4;                    // [kBlock]
+  uint32_t* wsum = lrc + kBlock;                       // [4]
+  const uint32_t f = blockIdx.y;
+  const int tid = threadIdx.x;
+  const uint32_t n = min(b.rec_count[f * kCounterStride], b.rec_cap);
+  const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
+  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
   __syncthreads();
-  const uint32_t nb = n_big;
-  for (uint32_t e = 0; e < nb; ++e) {
-    const uint32_t rc = big[e];
-    const uint32_t area = rect_area(rc);
-    for (uint32_t q = tid; q < area; q += kBlock) atomicAdd(&hist[rect_tile(rc, q, s.tiles_x)], 1u);
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t r = base + tid;
+    uint32_t area = 0;
+    if (r < n) {
+      const uint32_t rc = rect[r];
+      lrc[tid] = rc;
+      area = rect_area(rc);
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(area, wsum, total);
+    pre[tid] = ex;
+    if (tid == kBlock - 1) pre[kBlock] = ex + area;
+    __syncthreads();
+    for (uint32_t j = tid; j < total; j += kBlock) {
+      const int k = find_item(pre, j);
+      atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   uint32_t* tc = b.tile_count + (size_t)f * s.n_tiles;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) {
     const uint32_t c = hist[t];
@@ -441,7 +520,7 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   __shared__ uint32_t wsum[kBlock / 64];
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x;
-  const uint32_t n = min(b.rec_count[f], b.rec_cap);
+  const uint32_t n = min(b.rec_count[f * kCounterStride], b.rec_cap);
   const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
   uint32_t* fill = b.tile_fill + (size_t)f * s.n_tiles;
@@ -486,15 +565,240 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   }
 }
 
+// Conservative range [xl, xr] (tile-local, clamped to [x0, x1]) of pixels on row
+// `py` whose centres can pass the exact edge tests of R.  Each edge
+// E(cx) = c0 - dy*cx is solved for its boundary in float relative to the tile
+// origin (|error| << 1/16 px for any boundary that lands inside the tile);
+// a 1/16-px margin keeps the range a superset of the exact set, and the
+// per-pixel integer test decides coverage, so results never depend on it.
+__device__ __forceinline__ void row_span(const Rec& R, int ox, int py, int x0, int x1, int& xl, int& xr) {
+  const int32_t cy = py * 256 + 128;
+  const int32_t OX = ox * 256;
+  float lo = -1.0e30f, hi = 1.0e30f;
+  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
+    const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
+    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+    const int64_t c0 = (int64_t)dx * (cy - ay) + (int64_t)dy * (ax - OX) + bias;   // E = c0 - dy*(cx-OX)
+    if (dy == 0) {
+      if (c0 < 0) hi = -1.0e30f;
+    } else {
+      const float t = __fdividef((float)c0, (float)dy);   // approximate: covered by the margin
+      if (dy > 0) hi = fminf(hi, t); else lo = fmaxf(lo, t);
+    }
+  }
+  const float l = fminf(fmaxf((lo - 128.0f) * (1.0f / 256.0f) - 0.0625f, (float)x0 - 1.0f), (float)x1 + 1.0f);
+  const float h = fmaxf(fminf((hi - 128.0f) * (1.0f / 256.0f) + 0.0625f, (float)x1 + 1.0f), (float)x0 - 1.0f);
+  xl = max((int)ceilf(l), x0);
+  xr = min((int)floorf(h), x1);
+}
+
 // ---------------------------------------------------------------------------
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
+struct RasterCtx {
+  const SceneDev* s;
+  unsigned long long* zb;
+  int ox, oy;
+  float inv_near, inv_far;
+  uint32_t dbg;
+};
+
+// Exact per-pixel test of the spec for record R at pixel (ox+lx, oy+ly):
+// fixed-point edges with the top-left rule, homogeneous depth, depth range,
+// early-z against the LDS key, alpha test, then ds_min_u64.
+__device__ __forceinline__ void fragment(const RasterCtx& c, const Rec& R, int lx, int ly) {
+  const int px = c.ox + lx, py = c.oy + ly;
+  const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
+  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+  bool inside = true;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
+    const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
+    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+    const int64_t ev = (int64_t)dx * (cy - ay) - (int64_t)dy * (cx - ax);
+    inside &= (ev + bias) >= 0;
+  }
+  if (!inside) return;
+  float e[3], ssum, invw;
+  hom_eval(R.A, R.B, R.C, R.invdet, px, py, e, ssum, invw);
+  if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
+  const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | R.uid;
+  unsigned long long* z = &c.zb[ly * kTile + lx];
+  if (!(c.dbg & 16u) && key >= *z) return;
+  const MatDesc mat = c.s->mats[R.mat];
+  if (!(c.dbg & 4u) && mat.alpha_test && mat.texture >= 0) {
+    float u, v;
+    int cc[4];
+    interp_uv(e, ssum, R.uv, u, v);
+    tex_sample(*c.s, mat.texture, u, v, cc);
+    if (!(cc[3] > (int)mat.alpha_threshold)) return;
+  }
+  atomicMin(z, key);
+}
+
+__device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t* bins, uint32_t idx, uint32_t end,
+                                                 uint32_t rec_cap, Rec* slot, int ox, int oy, uint32_t& rect) {
+  uint32_t rows = 0;
+  rect = 0;
+  const uint32_t r = (idx < end) ? bins[idx] : 0xFFFFFFFFu;
+  if (r < rec_cap) {
+    const uint4* src = reinterpret_cast<const uint4*>(recs + r);
+    uint4* dst = reinterpret_cast<uint4*>(slot);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) dst[k] = src[k];
+    const Rec& R = *slot;
+    const int x0 = max((int)R.px0, ox) - ox, x1 = min((int)R.px1, ox + kTile - 1) - ox;
+    const int y0 = max((int)R.py0, oy) - oy, y1 = min((int)R.py1, oy + kTile - 1) - oy;
+    if (x0 <= x1 && y0 <= y1) {
+      rows = (uint32_t)(y1 - y0 + 1);
+      rect = (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)x1 << 16);
+    }
+  }
+  return rows;
+}
+
+struct RasterLds {
+  Rec lrec[kBlock];                 // 28 KiB staged bin records
+  uint32_t lrect[kBlock];
+  uint32_t pre[kBlock + 1];
+  uint32_t span[kBlock];
+  uint32_t pre2[kBlock + 1];
+  uint32_t wsum[kBlock / 64];
+};
+
+// V0/V2: block-level two-level expansion of 256-record batches.
+//   level 1: (record, row) items, one per thread -> conservative row span
+//   level 2: (span, pixel) items.  V0 finds each item's span by binary search;
+//            V2 gives every thread a contiguous run of items, searches once
+//            and walks (owner changes every ~3 items), keeping the record in
+//            registers while the owner's record is unchanged.
+template <int V>
+__device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds& L, uint32_t beg,
+                                             uint32_t end, const uint32_t* bins, const Rec* recs) {
+  const int tid = threadIdx.x;
+  for (uint32_t base = beg; base < end; base += kBlock) {
+    uint32_t rect;
+    const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, &L.lrec[tid], c.ox, c.oy, rect);
+    L.lrect[tid] = rect;
+    uint32_t tot1;
+    const uint32_t ex1 = block_excl_scan(rows, L.wsum, tot1);
+    L.pre[tid] = ex1;
+    if (tid == kBlock - 1) L.pre[kBlock] = ex1 + rows;
+    __syncthreads();
+    for (uint32_t c1 = 0; c1 < tot1; c1 += kBlock) {
+      const uint32_t j1 = c1 + tid;
+      uint32_t w2 = 0;
+      if (j1 < tot1) {
+        const int k = find_item(L.pre, j1);
+        const uint32_t rc = L.lrect[k];
+        const int ly = (int)((rc >> 8) & 255u) + (int)(j1 - L.pre[k]);
+        int xl, xr;
+        row_span(L.lrec[k], c.ox, c.oy + ly, (int)(rc & 255u), (int)((rc >> 16) & 255u), xl, xr);
+        if (xl <= xr) {
+          w2 = (uint32_t)(xr - xl + 1);
+          L.span[tid] = (uint32_t)k | ((uint32_t)ly << 8) | ((uint32_t)xl << 16);
+        }
+      }
+      uint32_t tot2;
+      const uint32_t ex2 = block_excl_scan(w2, L.wsum, tot2);
+      L.pre2[tid] = ex2;
+      if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
+      __syncthreads();
+      if constexpr (V == 0) {
+        for (uint32_t j = tid; j < ((b.dbg & 8u) ? 0u : tot2); j += kBlock) {
+          const int s2 = find_item(L.pre2, j);
+          const uint32_t sp = L.span[s2];
+          const int ly = (int)((sp >> 8) & 255u), lx = (int)((sp >> 16) & 255u) + (int)(j - L.pre2[s2]);
+          fragment(c, L.lrec[sp & 255u], lx, ly);
+        }
+      } else {
+        const uint32_t per = (tot2 + kBlock - 1) / kBlock;
+        uint32_t j = (uint32_t)tid * per;
+        const uint32_t jend = min(j + per, tot2);
+        if (j < jend) {
+          int s2 = find_item(L.pre2, j);
+          uint32_t sst = L.pre2[s2], snx = L.pre2[s2 + 1], sp = L.span[s2];
+          uint32_t k = sp & 255u;
+          Rec R = L.lrec[k];
+          for (; j < jend; ++j) {
+            while (j >= snx) {
+              ++s2;
+              sst = snx;
+              snx = L.pre2[s2 + 1];
+              sp = L.span[s2];
+              if ((sp & 255u) != k) {
+                k = sp & 255u;
+                R = L.lrec[k];
+              }
+            }
+            fragment(c, R, (int)((sp >> 16) & 255u) + (int)(j - sst), (int)((sp >> 8) & 255u));
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+struct WaveLds {
+  Rec lrec[kBlock];
+  uint32_t wmark[kBlock];
+};
+
+// V1: wave-level expansion (each wave owns 64 of every 256 records; owners
+// found by start marks + wave max-scan; no block barrier inside the loop).
+__device__ __forceinline__ void raster_wave(const RasterCtx& c, const BatchDev& b, WaveLds& L, uint32_t beg,
+                                            uint32_t end, const uint32_t* bins, const Rec* recs) {
+  const int tid = threadIdx.x;
+  const int wid = tid >> 6, lane = tid & 63;
+  Rec* wrec = &L.lrec[wid * 64];
+  uint32_t* mark = &L.wmark[wid * 64];
+  for (uint32_t base = beg + (uint32_t)wid * 64u; base < end; base += kBlock) {
+    uint32_t rect;
+    const uint32_t rows = stage_record(recs, bins, base + lane, end, b.rec_cap, &wrec[lane], c.ox, c.oy, rect);
+    wave_lds_sync();
+    const uint32_t inc1 = wave_incl_scan(rows);
+    const uint32_t st1 = inc1 - rows;
+    const uint32_t tot1 = __builtin_amdgcn_readlane(inc1, 63);
+    uint32_t carry1 = 0;
+    for (uint32_t w1 = 0; w1 < tot1; w1 += 64) {
+      const uint32_t own1 = window_owner(mark, lane, rows != 0, st1 - w1, carry1);
+      const uint32_t item1 = w1 + (uint32_t)lane;
+      const uint32_t o_st = __shfl(st1, (int)own1, 64), o_rect = __shfl(rect, (int)own1, 64);
+      uint32_t w2 = 0, sp = 0;
+      if (item1 < tot1) {
+        const int ly = (int)((o_rect >> 8) & 255u) + (int)(item1 - o_st);
+        int xl, xr;
+        row_span(wrec[own1], c.ox, c.oy + ly, (int)(o_rect & 255u), (int)((o_rect >> 16) & 255u), xl, xr);
+        if (xl <= xr) {
+          w2 = (uint32_t)(xr - xl + 1);
+          sp = own1 | ((uint32_t)ly << 8) | ((uint32_t)xl << 16);
+        }
+      }
+      const uint32_t inc2 = wave_incl_scan(w2);
+      const uint32_t st2 = inc2 - w2;
+      const uint32_t tot2 = __builtin_amdgcn_readlane(inc2, 63);
+      uint32_t carry2 = 0;
+      for (uint32_t w2b = 0; w2b < tot2; w2b += 64) {
+        const uint32_t own2 = window_owner(mark, lane, w2 != 0, st2 - w2b, carry2);
+        const uint32_t j = w2b + (uint32_t)lane;
+        const uint32_t o_sp = __shfl(sp, (int)own2, 64), o_st2 = __shfl(st2, (int)own2, 64);
+        if (j < tot2)
+          fragment(c, wrec[o_sp & 255u], (int)((o_sp >> 16) & 255u) + (int)(j - o_st2), (int)((o_sp >> 8) & 255u));
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
+template <int V>
 __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
   __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
-  __shared__ Rec lrec[kBlock];                       // 28 KiB staged bin records
-  __shared__ uint32_t lrect[kBlock];
-  __shared__ uint32_t pre[kBlock + 1];
-  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ typename std::conditional<V == 1, WaveLds, RasterLds>::type L;
   __shared__ uint32_t lstat[5][kMaxLdsLabels];
   const int tid = threadIdx.x;
   const uint32_t tile = blockIdx.x, f = blockIdx.y;
@@ -505,74 +809,21 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
     lstat[0][l] = 0; lstat[1][l] = 0xFFFFFFFFu; lstat[2][l] = 0xFFFFFFFFu; lstat[3][l] = 0; lstat[4][l] = 0;
   }
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
-  const uint32_t beg = min(toff[tile], b.bin_cap), end = min(toff[tile + 1], b.bin_cap);
+  const uint32_t beg = min(toff[tile], b.bin_cap);
+  const uint32_t end = (b.dbg & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
   const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
-  const float inv_near = 1.0f / s.near_clip, inv_far = 1.0f / s.far_clip;
+  RasterCtx c{&s, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg};
+  __syncthreads();
+  if constexpr (V == 1) raster_wave(c, b, L, beg, end, bins, recs);
+  else raster_block<V>(c, b, L, beg, end, bins, recs);
   __syncthreads();
 
-  for (uint32_t base = beg; base < end; base += kBlock) {
-    const uint32_t idx = base + tid;
-    uint32_t area = 0;
-    const uint32_t r = (idx < end) ? bins[idx] : 0xFFFFFFFFu;
-    if (r < b.rec_cap) {
-      const uint4* src = reinterpret_cast<const uint4*>(recs + r);
-      uint4* dst = reinterpret_cast<uint4*>(&lrec[tid]);
-#pragma unroll
-      for (int k = 0; k < 7; ++k) dst[k] = src[k];
-      const Rec& R = lrec[tid];
-      const int x0 = max((int)R.px0, ox) - ox, x1 = min((int)R.px1, ox + kTile - 1) - ox;
-      const int y0 = max((int)R.py0, oy) - oy, y1 = min((int)R.py1, oy + kTile - 1) - oy;
-      if (x0 <= x1 && y0 <= y1) {
-        const uint32_t w = (uint32_t)(x1 - x0 + 1), hh = (uint32_t)(y1 - y0 + 1);
-        area = w * hh;
-        lrect[tid] = (uint32_t)x0 | ((uint32_t)y0 << 8) | (w << 16);
-      }
-    }
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(area, wsum, total);
-    pre[tid] = ex;
-    if (tid == kBlock - 1) pre[kBlock] = ex + area;
+  if (b.dbg & 1u) {   // ablation: keep the raster loop alive, skip the resolve
     __syncthreads();
-    for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_item(pre, j);
-      const uint32_t q = j - pre[k];
-      const uint32_t rc = lrect[k];
-      const uint32_t w = rc >> 16;
-      const int lx = (int)(rc & 255u) + (int)(q % w), ly = (int)((rc >> 8) & 255u) + (int)(q / w);
-      const int px = ox + lx, py = oy + ly;
-      const Rec& R = lrec[k];
-      const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
-      const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
-      bool inside = true;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
-        const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
-        const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-        const int64_t ev = (int64_t)dx * (cy - ay) - (int64_t)dy * (cx - ax);
-        inside &= (ev + bias) >= 0;
-      }
-      if (!inside) continue;
-      float e[3], ssum, invw;
-      hom_eval(R.A, R.B, R.C, R.invdet, px, py, e, ssum, invw);
-      if (!(invw >= inv_far && invw <= inv_near)) continue;
-      const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | R.uid;
-      unsigned long long* z = &zb[ly * kTile + lx];
-      if (key >= *z) continue;
-      const MatDesc mat = s.mats[R.mat];
-      if (mat.alpha_test && mat.texture >= 0) {
-        float u, v;
-        int c[4];
-        interp_uv(e, ssum, R.uv, u, v);
-        tex_sample(s, mat.texture, u, v, c);
-        if (!(c[3] > (int)mat.alpha_threshold)) continue;
-      }
-      atomicMin(z, key);
-    }
-    __syncthreads();
+    if (tid == 0 && zb[0] == 0ull && b.inst) b.inst[0] = 0;
+    return;
   }
-
   // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads
   const int ly = tid >> 3, lx0 = (tid & 7) * 4;
   const int py = oy + ly;
@@ -739,6 +990,267 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// per-pixel resolve (shared by the raster kernels)
+// ---------------------------------------------------------------------------
+struct ResolveCache {
+  uint32_t uid = 0xFFFFFFFFu;
+  Hom h;
+  float uvv[6];
+  int32_t label = -1;
+  int tex = -1;
+  int base[3] = {0, 0, 0};
+  int q[3] = {0, 0, 0};
+};
+
+// Shade one pixel from its winning (depth, uid) key: depth, instance id and
+// RGB exactly as csg_oracle.c's resolve (recomputes the triangle's clip
+// coordinates; cached across pixels of the same triangle).
+__device__ __forceinline__ void resolve_pixel(const SceneDev& s, const BatchDev& b, uint32_t f, int px, int py,
+                                              unsigned long long key, ResolveCache& rc, uint32_t& rgb_out,
+                                              int32_t& id_out, float& depth_out) {
+  if (key == kEmptyKey) {
+    rgb_out = s.sky & 0xFFFFFFu;
+    id_out = -1;
+    depth_out = INFINITY;
+    return;
+  }
+  const uint32_t uid = (uint32_t)key;
+  const uint32_t i = uid >> kUidShift, t = uid & (kMaxTrisPerMesh - 1u);
+  if (uid != rc.uid) {
+    rc.uid = uid;
+    const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
+    float c[12];
+#pragma unroll
+    for (int z = 0; z < 12; ++z) c[z] = Cm[z];
+    const MeshDesc m = s.meshes[s.inst_mesh[i]];
+    const uint32_t* tri = s.tris + (size_t)(m.tbase + t) * 3;
+    float pobj[3][3];
+    Cv3 v[3];
+#pragma unroll
+    for (int z = 0; z < 3; ++z) {
+      const float* p = s.pos + (size_t)(m.vbase + tri[z]) * 3;
+      pobj[z][0] = p[0]; pobj[z][1] = p[1]; pobj[z][2] = p[2];
+      v[z].x = dot4(c + 0, p[0], p[1], p[2]);
+      v[z].y = dot4(c + 4, p[0], p[1], p[2]);
+      v[z].w = dot4(c + 8, p[0], p[1], p[2]);
+    }
+    hom_setup(v, rc.h);
+    rc.label = s.inst_label[i];
+    const MatDesc mat = s.mats[m.material];
+    rc.tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
+    rc.base[0] = mat.base[0]; rc.base[1] = mat.base[1]; rc.base[2] = mat.base[2];
+    if (rc.tex >= 0) {
+      const uint32_t* ut = s.uv_tris + (size_t)(m.tbase + t) * 3;
+#pragma unroll
+      for (int z = 0; z < 3; ++z) {
+        const float* uq = s.uvs + (size_t)(m.uvbase + ut[z]) * 2;
+        rc.uvv[2 * z] = uq[0];
+        rc.uvv[2 * z + 1] = uq[1];
+      }
+    }
+    const float* M = b.models + ((size_t)b.frames[f].xform_set * s.n_inst + i) * 16;
+    float mm[12];
+#pragma unroll
+    for (int z = 0; z < 12; ++z) mm[z] = M[z];
+    float pw[3][3];
+#pragma unroll
+    for (int z = 0; z < 3; ++z) {
+      pw[z][0] = dot4(mm + 0, pobj[z][0], pobj[z][1], pobj[z][2]);
+      pw[z][1] = dot4(mm + 4, pobj[z][0], pobj[z][1], pobj[z][2]);
+      pw[z][2] = dot4(mm + 8, pobj[z][0], pobj[z][1], pobj[z][2]);
+    }
+    const float e1x = pw[1][0] - pw[0][0], e1y = pw[1][1] - pw[0][1], e1z = pw[1][2] - pw[0][2];
+    const float e2x = pw[2][0] - pw[0][0], e2y = pw[2][1] - pw[0][1], e2z = pw[2][2] - pw[0][2];
+    const float nx = e1y * e2z - e1z * e2y;
+    const float ny = e1z * e2x - e1x * e2z;
+    const float nz = e1x * e2y - e1y * e2x;
+    const float nn = (nx * nx + ny * ny) + nz * nz;
+    float cs = 0.0f;
+    if (nn > 0.0f) {
+      const float d = (nx * s.sun_dir[0] + ny * s.sun_dir[1]) + nz * s.sun_dir[2];
+      cs = fabsf(d / sqrtf(nn));
+    }
+#pragma unroll
+    for (int z = 0; z < 3; ++z) {
+      const float shade = s.ambient[z] + s.sun[z] * cs;
+      const int qq = (int)(shade * 256.0f + 0.5f);
+      rc.q[z] = min(max(qq, 0), 65535);
+    }
+  }
+  float e[3], ssum, invw;
+  hom_eval(rc.h.A, rc.h.B, rc.h.C, rc.h.invdet, px, py, e, ssum, invw);
+  depth_out = 1.0f / invw;
+  id_out = rc.label;
+  int alb[3];
+  if (rc.tex >= 0) {
+    float u, v;
+    int c[4];
+    interp_uv(e, ssum, rc.uvv, u, v);
+    tex_sample(s, rc.tex, u, v, c);
+#pragma unroll
+    for (int z = 0; z < 3; ++z) alb[z] = (c[z] * rc.base[z] + 127) / 255;
+  } else {
+#pragma unroll
+    for (int z = 0; z < 3; ++z) alb[z] = rc.base[z];
+  }
+  uint32_t o = 0;
+#pragma unroll
+  for (int z = 0; z < 3; ++z) o |= (uint32_t)min((alb[z] * rc.q[z] + 128) >> 8, 255) << (8 * z);
+  rgb_out = o;
+}
+
+// ---------------------------------------------------------------------------
+// k_raster_px: pixel-parallel tile raster (V3).  One wave per 32x32 tile;
+// lane l owns pixel (l & 7, l >> 3) of each of the tile's sixteen 8x8 blocks
+// and keeps their (depth, uid) keys in registers.  The wave walks the tile's
+// bin; each record is read with wave-uniform (scalar) loads, its bbox picks
+// the blocks it can touch, one wave instruction stream tests 64 pixels of a
+// block at once, and a ballot skips blocks the triangle misses.  No LDS
+// z-buffer, no atomics, no scans, no barriers in the raster loop.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_raster_px(SceneDev s, BatchDev b) {
+  __shared__ uint32_t o_rgb[kTilePix];
+  __shared__ int32_t o_id[kTilePix];
+  __shared__ float o_dep[kTilePix];
+  const int lane = threadIdx.x;
+  const uint32_t tile = blockIdx.x, f = blockIdx.y;
+  const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
+  const int lxo = lane & 7, lyo = lane >> 3;
+  const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
+  const uint32_t beg = min(toff[tile], b.bin_cap);
+  const uint32_t end = (b.dbg & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
+  const uint32_t* __restrict__ bins = b.bins + (size_t)f * b.bin_cap;
+  const Rec* __restrict__ recs = b.recs + (size_t)f * b.rec_cap;
+  const float inv_near = 1.0f / s.near_clip, inv_far = 1.0f / s.far_clip;
+  unsigned long long zk[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) zk[k] = kEmptyKey;
+
+  for (uint32_t i = beg; i < end; ++i) {
+    const uint32_t ri = __builtin_amdgcn_readfirstlane(bins[i]);
+    if (ri >= b.rec_cap) continue;
+    const Rec& R = recs[ri];
+    const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+    int32_t ax[3], ay[3], dx[3], dy[3], bias[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      ax[e] = R.x[ea[e]];
+      ay[e] = R.y[ea[e]];
+      dx[e] = R.x[eb[e]] - ax[e];
+      dy[e] = R.y[eb[e]] - ay[e];
+      bias[e] = (dy[e] < 0 || (dy[e] == 0 && dx[e] > 0)) ? 0 : -1;
+    }
+    const int bx0 = ((int)R.px0 - ox) >> 3, bx1 = ((int)R.px1 - ox) >> 3;
+    const int by0 = ((int)R.py0 - oy) >> 3, by1 = ((int)R.py1 - oy) >> 3;
+    const float A0 = R.A[0], A1 = R.A[1], A2 = R.A[2], B0 = R.B[0], B1 = R.B[1], B2 = R.B[2];
+    const float C0 = R.C[0], C1 = R.C[1], C2 = R.C[2], invdet = R.invdet;
+    const uint32_t uid = R.uid;
+    const MatDesc mat = s.mats[R.mat];
+    const bool alpha = mat.alpha_test && mat.texture >= 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int bx = k & 3, by = k >> 2;
+      if (bx < bx0 || bx > bx1 || by < by0 || by > by1) continue;       // uniform
+      const int px = ox + bx * 8 + lxo, py = oy + by * 8 + lyo;
+      const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
+      bool inside = px <= (int)R.px1 && py <= (int)R.py1 && px >= (int)R.px0 && py >= (int)R.py0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const int64_t ev = (int64_t)dx[e] * (cy - ay[e]) - (int64_t)dy[e] * (cx - ax[e]);
+        inside &= (ev + bias[e]) >= 0;
+      }
+      if (__ballot(inside) == 0) continue;                              // wave-uniform skip
+      if (!inside) continue;
+      const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+      const float e0 = (A0 * fx + B0 * fy) + C0;
+      const float e1 = (A1 * fx + B1 * fy) + C1;
+      const float e2 = (A2 * fx + B2 * fy) + C2;
+      const float ssum = (e0 + e1) + e2;
+      const float invw = ssum * invdet;
+      if (!(invw >= inv_far && invw <= inv_near)) continue;
+      const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | uid;
+      if (key >= zk[k]) continue;
+      if (alpha && !(b.dbg & 4u)) {
+        const float ee[3] = {e0, e1, e2};
+        float u, v;
+        int cc[4];
+        interp_uv(ee, ssum, R.uv, u, v);
+        tex_sample(s, mat.texture, u, v, cc);
+        if (!(cc[3] > (int)mat.alpha_threshold)) continue;
+      }
+      zk[k] = key;
+    }
+  }
+  if (b.dbg & 1u) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc ^= zk[k];
+    if (acc == 0x1234ull && b.inst) b.inst[0] = 0;
+    return;
+  }
+  // resolve into LDS (tile-linear), then coalesced row stores
+  ResolveCache rc;
+  const uint32_t nl = b.stats ? b.n_labels : 0u;
+  uint32_t* stf = b.stats ? b.stats + (size_t)f * b.n_labels * 5 : nullptr;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int lx = (k & 3) * 8 + lxo, ly = (k >> 2) * 8 + lyo;
+    const int px = ox + lx, py = oy + ly;
+    uint32_t rgb = 0;
+    int32_t id = -1;
+    float dep = INFINITY;
+    if (px < (int)s.W && py < (int)s.H) {
+      resolve_pixel(s, b, f, px, py, zk[k], rc, rgb, id, dep);
+      if (id >= 0 && (uint32_t)id < nl) {
+        atomicAdd(&stf[id * 5 + 0], 1u);
+        atomicMin(&stf[id * 5 + 1], (uint32_t)px);
+        atomicMin(&stf[id * 5 + 2], (uint32_t)py);
+        atomicMax(&stf[id * 5 + 3], (uint32_t)px);
+        atomicMax(&stf[id * 5 + 4], (uint32_t)py);
+      }
+    }
+    o_rgb[ly * kTile + lx] = rgb;
+    o_id[ly * kTile + lx] = id;
+    o_dep[ly * kTile + lx] = dep;
+  }
+  __syncthreads();
+  const size_t npx = (size_t)s.W * s.H;
+  // 32 rows x 32 px: each lane stores 4 consecutive pixels of a row per step
+#pragma unroll
+  for (int step = 0; step < 4; ++step) {
+    const int q = step * 64 + lane;          // 256 quads of 4 pixels
+    const int ly = q >> 3, lx = (q & 7) * 4;
+    const int py = oy + ly, px = ox + lx;
+    if (py >= (int)s.H) continue;
+    const size_t o = (size_t)f * npx + (size_t)py * s.W + px;
+    const int t = ly * kTile + lx;
+    if (px + 3 < (int)s.W) {
+      if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(o_id[t], o_id[t + 1], o_id[t + 2], o_id[t + 3]);
+      if (b.depth)
+        *reinterpret_cast<float4*>(b.depth + o) = make_float4(o_dep[t], o_dep[t + 1], o_dep[t + 2], o_dep[t + 3]);
+      if (b.rgb) {
+        const uint32_t c0 = o_rgb[t], c1 = o_rgb[t + 1], c2 = o_rgb[t + 2], c3 = o_rgb[t + 3];
+        uint32_t* d = reinterpret_cast<uint32_t*>(b.rgb + o * 3);
+        d[0] = c0 | (c1 << 24);
+        d[1] = (c1 >> 8) | (c2 << 16);
+        d[2] = (c2 >> 16) | (c3 << 8);
+      }
+    } else {
+      for (int k = 0; k < 4 && px + k < (int)s.W; ++k) {
+        if (b.inst) b.inst[o + k] = o_id[t + k];
+        if (b.depth) b.depth[o + k] = o_dep[t + k];
+        if (b.rgb) {
+          const uint32_t cpx = o_rgb[t + k];
+          b.rgb[(o + k) * 3 + 0] = (uint8_t)(cpx & 255u);
+          b.rgb[(o + k) * 3 + 1] = (uint8_t)((cpx >> 8) & 255u);
+          b.rgb[(o + k) * 3 + 2] = (uint8_t)((cpx >> 16) & 255u);
+        }
+      }
+    }
+  }
+}
+
 __global__ void k_init_stats(uint32_t* st, uint32_t n) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) {
@@ -810,7 +1322,12 @@ void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t s
 void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks, uint32_t F,
                   hipStream_t st) {
   dim3 g(n_chunks, F);
-  hipLaunchKernelGGL(k_setup, g, dim3(kBlock), s.n_tiles * sizeof(uint32_t), st, s, b, chunks);
+  hipLaunchKernelGGL(k_setup, g, dim3(kBlock), 0, st, s, b, chunks);
+}
+
+void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+  const size_t lds = (((s.n_tiles + 3u) & ~3u) + 3 * kBlock + 12) * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_count, dim3(64, F), dim3(kBlock), lds, st, s, b);
 }
 
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
@@ -822,9 +1339,12 @@ void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st
   hipLaunchKernelGGL(k_bin, g, dim3(kBlock), 2 * s.n_tiles * sizeof(uint32_t), st, s, b);
 }
 
-void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st, int variant) {
   dim3 g(s.n_tiles, F);
-  hipLaunchKernelGGL(k_raster, g, dim3(kBlock), 0, st, s, b);
+  if (variant == 0) hipLaunchKernelGGL(k_raster<0>, g, dim3(kBlock), 0, st, s, b);
+  else if (variant == 1) hipLaunchKernelGGL(k_raster<1>, g, dim3(kBlock), 0, st, s, b);
+  else if (variant == 2) hipLaunchKernelGGL(k_raster<2>, g, dim3(kBlock), 0, st, s, b);
+  else hipLaunchKernelGGL(k_raster_px, g, dim3(64), 0, st, s, b);
 }
 
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st) {

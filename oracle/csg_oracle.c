@@ -173,6 +173,7 @@ static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3],
   if (py1 > H - 1) py1 = H - 1;
   if (px0 > px1 || py0 > py1) return;
   st->n_raster_tris++;
+  st->n_bbox_pixels += (uint64_t)(px1 - px0 + 1) * (uint64_t)(py1 - py0 + 1);
   static const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
   int32_t dx[3], dy[3];
   int bias[3];
@@ -192,14 +193,16 @@ static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3],
         if (e + bias[k] < 0) { inside = 0; break; }
       }
       if (!inside) continue;
+      st->n_covered++;
       float e[3], ssum, invw;
       hom_eval(h, px, py, e, &ssum, &invw);
       if (!(invw >= inv_far && invw <= inv_near)) continue;
       st->n_fragments++;
       const uint64_t key = ((uint64_t)(0xFFFFFFFFu - fbits(invw)) << 32) | uid;
       uint64_t* z = &zbuf[(size_t)py * W + px];
-      if (key >= *z) continue;
+      if (key >= *z) { st->n_early_z_killed++; continue; }
       if (mat->alpha_test && mat->texture >= 0) {
+        st->n_alpha_tests++;
         float u, v;
         int c[4];
         interp_uv(e, ssum, uv, &u, &v);

@@ -65,6 +65,7 @@ typedef struct {
 
 typedef struct {
   uint64_t n_tris_in, n_culled, n_clipped, n_raster_tris, n_fragments, n_alpha_killed;
+  uint64_t n_bbox_pixels, n_covered, n_early_z_killed, n_alpha_tests;
 } oracle_stats;
 
 /* Render one frame. view/proj: 16 floats row-major (proj rows 0,1,3 used).

@@ -35,7 +35,8 @@ class _Scene(C.Structure):
 
 class _Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("n_tris_in", "n_culled", "n_clipped", "n_raster_tris",
-                                           "n_fragments", "n_alpha_killed")]
+                                           "n_fragments", "n_alpha_killed", "n_bbox_pixels", "n_covered",
+                                           "n_early_z_killed", "n_alpha_tests")]
 
 
 def build() -> str:
