@@ -1,0 +1,95 @@
+"""The reference-shaped boundary (Camera / AnnotatorRegistry / next_update)
+and the batched generator, on the GPU, checked against the CPU oracle."""
+import asyncio
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def stage():
+    from constructionsceneposeestimation_amd import sensors
+    sensors.reset()
+    st = sensors.Stage("C3", seed=2)
+    yield st
+    sensors.reset()
+
+
+def test_camera_annotator_loop_matches_oracle(stage):
+    """The reference's loop shape (generate_construction_data.py:1540-2072)
+    driven through the shim; every output checked against the oracle."""
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd import sensors
+    from constructionsceneposeestimation_amd.annotators import AnnotatorRegistry
+    from constructionsceneposeestimation_amd.labels import bboxDict_to_transform
+    from constructionsceneposeestimation_amd.packing import pack_scene
+    from oracle.oracle import Oracle
+
+    W, H = 320, 180
+    cam = sensors.Camera("/World/Camera_0", resolution=(W, H), stage=stage)
+    cam.initialize()
+    ann = {n: AnnotatorRegistry.get_annotator(n) for n in
+           ("distance_to_image_plane", "instance_segmentation", "bounding_box_3d", "pointcloud")}
+    for a in ann.values():
+        a.attach(cam.get_render_product_path())
+    o = Oracle(pack_scene(stage.scene), W, H)
+    for k, (pos, aim) in enumerate([([-3, -3, 1.6], [0, 0, 1.6]), ([6, 0, 2.5], [0, 0, 2.5])]):
+        if k == 1:
+            moved = stage.randomize_object_positions()
+            assert moved and {"path", "new_pos", "rotation", "type", "no_overlap"} <= set(moved[0])
+        cam.set_world_pose(position=np.array(pos, float), orientation=cm.look_at_world_quat(pos, aim))
+        asyncio.run(sensors.next_update_async())
+        rgba = cam.get_rgba()
+        assert rgba.shape == (H, W, 4) and rgba.dtype == np.uint8
+        depth = ann["distance_to_image_plane"].get_data()
+        inst = ann["instance_segmentation"].get_data()
+        boxes = ann["bounding_box_3d"].get_data()
+        pcd = ann["pointcloud"].get_data()
+        o.set_instance_models(stage.state.models.reshape(-1, 16))
+        V, P, C = cm.frame_matrices(pos, cm.look_at_world_quat(pos, aim), cam.intrinsics())
+        ref = o.render(V, P)
+        assert np.array_equal(rgba[..., :3], ref["rgb"])
+        assert np.array_equal(depth.view(np.uint32), ref["depth"].view(np.uint32))
+        ids = np.where(ref["instance"] >= 0, ref["instance"] + 1, 0)
+        assert np.array_equal(inst["data"], ids.astype(np.uint32))
+        assert set(inst["info"]["idToLabels"]) == set(np.unique(ids[ids > 0]).tolist())
+        # bbox_3d records are consumable by the reference's own conversion
+        assert len(boxes["info"]["primPaths"]) == len(boxes["data"]) > 0
+        for rec in boxes["data"]:
+            c, s, e = bboxDict_to_transform(tuple(rec))
+            assert all(np.isfinite(c)) and all(x >= 0 for x in s)
+        # point cloud: one point per finite depth pixel, on the camera ray
+        assert pcd["data"].shape == (int(np.isfinite(depth).sum()), 3)
+        camp = np.asarray(cam.get_obj_pose()[:3])
+        dist = np.linalg.norm(pcd["data"] - camp, axis=1)
+        assert np.all(dist >= depth[np.isfinite(depth)] - 1e-3)
+        pose = stage.get_obj_pose("/World/Camera_0")
+        np.testing.assert_allclose(pose[:3], pos, atol=1e-9)
+
+
+def test_generate_writes_reference_layout(tmp_path):
+    from constructionsceneposeestimation_amd.generate import generate
+    summary = generate(str(tmp_path), list(range(12)), "C3", seed=1, batch=5, width=160, height=96,
+                       depth=True, pointcloud=True)
+    assert summary["counters"]["successful_frames"] == 12
+    lab = json.load(open(tmp_path / "labels" / "label_000011.json"))
+    assert {"frame_id", "camera_pose", "camera_params", "objects", "instance_mask_shape", "num_objects",
+            "class_mapping"} <= set(lab)
+    assert lab["instance_mask_shape"] == [96, 160] and len(lab["camera_pose"]) == 7
+    m = np.load(tmp_path / "labels" / "instance_mask_000011.npy")
+    assert m.dtype == np.int32 and m.shape == (96, 160)
+    vis = {o["inst_idx"] for o in lab["objects"]}
+    assert vis == set(np.unique(m[m >= 0]).tolist())
+    for o in lab["objects"]:
+        assert {"inst_idx", "class_id", "class_name", "center", "size", "rotation", "prim_path",
+                "bbox_2d", "pixel_count", "keypoints_2d"} <= set(o)
+    assert os.path.exists(tmp_path / "rgb" / "rgb_000000.png")
+    assert os.path.exists(tmp_path / "pointcloud" / "pointcloud_000003.txt")
+    assert os.path.exists(tmp_path / "logs" / "generation_summary.json")
+    # resume: nothing left to do
+    again = generate(str(tmp_path), list(range(12)), "C3", seed=1, batch=5, width=160, height=96)
+    assert again["counters"]["total_attempts"] == 0
