@@ -11,6 +11,7 @@ from typing import Optional
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcsg.so")
+ABI_VERSION = 1  # CSG_ABI_VERSION in include/csg_api.h
 
 EXPORTED = (
     "csg_create", "csg_destroy", "csg_last_error", "csg_abi_version", "csg_upload_scene",
@@ -111,5 +112,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib.csg_project_keypoints.argtypes = [vp, vp, u32, vp, vp, vp, vp]
     lib.csg_timing_reset.argtypes = [vp]
     lib.csg_timing_read.argtypes = [vp, C.POINTER(Timing)]
+    if lib.csg_abi_version() != ABI_VERSION:
+        raise CsgError(f"libcsg.so ABI {lib.csg_abi_version()} != binding ABI {ABI_VERSION}; rebuild")
     _lib = lib
     return lib

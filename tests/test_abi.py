@@ -70,3 +70,9 @@ def test_frame_dtype_matches_abi():
     from constructionsceneposeestimation_amd import _lib
     from constructionsceneposeestimation_amd.renderer import FRAME_DTYPE
     assert FRAME_DTYPE.itemsize == C.sizeof(_lib.Frame) == 136
+
+
+def test_abi_version_matches_header():
+    from constructionsceneposeestimation_amd import _lib
+    m = re.search(r"#define\s+CSG_ABI_VERSION\s+(\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _lib.ABI_VERSION == _lib.load().csg_abi_version()
