@@ -63,10 +63,8 @@ struct csg_ctx {
   bool have_scene = false;
   uint32_t n_inst = 0, n_meshes = 0, n_materials = 0;
   uint64_t n_tris_total = 0;
-  DevBuf<float> pos, uvs;
-  DevBuf<uint32_t> tris, uv_tris, inst_mesh;
-  DevBuf<int32_t> inst_label;
-  DevBuf<MeshDesc> meshes;
+  DevBuf<float> tri_pos, tri_uv;       // de-indexed triangle soup (see SceneDev)
+  DevBuf<InstDesc> inst;
   DevBuf<MatDesc> mats;
   std::vector<MatDesc> h_mats;
   std::vector<MeshDesc> h_meshes;
@@ -169,8 +167,8 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
 void csg_destroy(csg_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  c->pos.release(); c->uvs.release(); c->tris.release(); c->uv_tris.release(); c->inst_mesh.release();
-  c->inst_label.release(); c->meshes.release(); c->mats.release(); c->chunks.release(); c->texels.release();
+  c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->mats.release(); c->chunks.release();
+  c->texels.release();
   c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
   c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
   c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
@@ -223,15 +221,27 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
     mats[k].alpha_test = materials[k].alpha_test;
     mats[k].alpha_threshold = materials[k].alpha_threshold;
   }
-  std::vector<uint32_t> imesh(n_inst), chunk_inst;
-  std::vector<int32_t> ilabel(n_inst);
+  // de-index: one 9-float position record and one 6-float uv record per triangle
+  const size_t n_soup = tris.size() / 3;
+  std::vector<float> tri_pos(n_soup * 9), tri_uv(n_soup * 6, 0.f);
+  for (uint32_t m = 0; m < n_meshes; ++m) {
+    const MeshDesc& d = md[m];
+    for (uint32_t t = 0; t < d.ntris; ++t) {
+      const size_t g = (size_t)d.tbase + t;
+      for (int k = 0; k < 3; ++k) {
+        memcpy(&tri_pos[g * 9 + 3 * k], &pos[((size_t)d.vbase + tris[g * 3 + k]) * 3], 3 * sizeof(float));
+        if (d.has_uv) memcpy(&tri_uv[g * 6 + 2 * k], &uvs[((size_t)d.uvbase + uvt[g * 3 + k]) * 2], 2 * sizeof(float));
+      }
+    }
+  }
+  std::vector<InstDesc> idesc(n_inst);
   std::vector<Chunk> ch;
   std::vector<float> models((size_t)n_inst * 16);
   uint64_t ntot = 0;
   for (uint32_t i = 0; i < n_inst; ++i) {
     if (inst[i].mesh >= n_meshes) return c->fail(CSG_ERR_INVALID, "instance %u: mesh out of range", i);
-    imesh[i] = inst[i].mesh;
-    ilabel[i] = inst[i].inst_idx;
+    const MeshDesc& mi = md[inst[i].mesh];
+    idesc[i] = InstDesc{mi.tbase, mi.material, mi.has_uv, inst[i].inst_idx};
     memcpy(&models[(size_t)i * 16], inst[i].model, 16 * sizeof(float));
     const uint32_t nt = md[inst[i].mesh].ntris;
     const MeshDesc& md_i = md[inst[i].mesh];
@@ -251,23 +261,15 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
     ntot += nt;
   }
   if (ch.empty()) return c->fail(CSG_ERR_INVALID, "upload_scene: no triangles");
-  HIP_TRY(c, c->pos.alloc(pos.size()));
-  HIP_TRY(c, c->uvs.alloc(uvs.size()));
-  HIP_TRY(c, c->tris.alloc(tris.size()));
-  HIP_TRY(c, c->uv_tris.alloc(uvt.size()));
-  HIP_TRY(c, c->meshes.alloc(n_meshes));
+  HIP_TRY(c, c->tri_pos.alloc(std::max<size_t>(tri_pos.size(), 9)));
+  HIP_TRY(c, c->tri_uv.alloc(std::max<size_t>(tri_uv.size(), 6)));
   HIP_TRY(c, c->mats.alloc(n_materials));
-  HIP_TRY(c, c->inst_mesh.alloc(n_inst));
-  HIP_TRY(c, c->inst_label.alloc(n_inst));
+  HIP_TRY(c, c->inst.alloc(n_inst));
   HIP_TRY(c, c->chunks.alloc(ch.size()));
-  HIP_TRY(c, hipMemcpy(c->pos.p, pos.data(), pos.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->uvs.p, uvs.data(), uvs.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->tris.p, tris.data(), tris.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->uv_tris.p, uvt.data(), uvt.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->meshes.p, md.data(), md.size() * sizeof(MeshDesc), hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->tri_pos.p, tri_pos.data(), tri_pos.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->tri_uv.p, tri_uv.data(), tri_uv.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->mats.p, mats.data(), mats.size() * sizeof(MatDesc), hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->inst_mesh.p, imesh.data(), imesh.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->inst_label.p, ilabel.data(), ilabel.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->inst.p, idesc.data(), idesc.size() * sizeof(InstDesc), hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->chunks.p, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice));
   c->n_inst = n_inst;
   c->n_meshes = n_meshes;
@@ -402,7 +404,8 @@ static int ensure_work(csg_ctx* c, uint32_t F) {
   HIP_TRY(c, c->tile_off.alloc((size_t)maxF * (c->n_tiles + 1)));
   HIP_TRY(c, c->tile_fill.alloc((size_t)maxF * c->n_tiles));
   HIP_TRY(c, c->bins.alloc((size_t)maxF * c->bin_cap));
-  HIP_TRY(c, c->overflow.alloc(1));
+  HIP_TRY(c, c->overflow.alloc(16));
+  HIP_TRY(c, hipMemset(c->overflow.p, 0, 16 * sizeof(uint32_t)));
   (void)npx;
   c->work_frames = maxF;
   return CSG_OK;
@@ -410,9 +413,8 @@ static int ensure_work(csg_ctx* c, uint32_t F) {
 
 static SceneDev scene_dev(const csg_ctx* c) {
   SceneDev s{};
-  s.pos = c->pos.p; s.tris = c->tris.p; s.uvs = c->uvs.p; s.uv_tris = c->uv_tris.p;
-  s.meshes = c->meshes.p; s.mats = c->mats.p; s.texd = c->texd.p; s.texels = c->texels.p;
-  s.inst_mesh = c->inst_mesh.p; s.inst_label = c->inst_label.p; s.n_inst = c->n_inst;
+  s.tri_pos = c->tri_pos.p; s.tri_uv = c->tri_uv.p; s.inst = c->inst.p;
+  s.mats = c->mats.p; s.texd = c->texd.p; s.texels = c->texels.p; s.n_inst = c->n_inst;
   for (int k = 0; k < 3; ++k) { s.ambient[k] = c->ambient[k]; s.sun[k] = c->sun[k]; s.sun_dir[k] = c->sun_dir[k]; }
   s.sky = c->sky;
   s.W = c->cfg.width; s.H = c->cfg.height;
@@ -545,6 +547,11 @@ int csg_synchronize(csg_ctx* c) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   uint32_t ov = 0;
   if (c->overflow.p) HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
+  if ((c->dbg & 512u) && c->overflow.p) {   // profiling counters, cumulative since the work buffers were sized
+    uint32_t ctr[16];
+    HIP_TRY(c, hipMemcpy(ctr, c->overflow.p, sizeof(ctr), hipMemcpyDeviceToHost));
+    fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u\n", ctr[1], ctr[2], ctr[3], ctr[4]);
+  }
   if (ov)
     return c->fail(CSG_ERR_OVERFLOW, "work buffer overflow (flags %u): records_per_frame=%u bins_per_frame=%u", ov,
                    c->rec_cap, c->bin_cap);

@@ -14,8 +14,11 @@ constexpr uint32_t kMaxInstances = 1u << (32 - kUidShift);
 constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
 constexpr int kMaxLdsLabels = 256;        // per-label pixel stats kept in LDS
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
+constexpr uint32_t kNoAlpha = 0xFFFFFFFFu;  // Rec::atex of a record without alpha test
 
-struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };
+struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };   // host-side bookkeeping
+// Per instance, everything a kernel needs before touching its triangles (one load).
+struct InstDesc { uint32_t tbase, material, has_uv; int32_t label; };
 struct MatDesc { uint8_t base[4]; int32_t texture; uint32_t alpha_test, alpha_threshold; };
 struct TexDesc { uint32_t offset, width, height, pad; };
 struct Chunk {                    // <= 256 triangles of one instance + their object-space AABB
@@ -31,11 +34,12 @@ struct __attribute__((aligned(16))) Rec {
   int32_t x[3], y[3];          // 24: 24.8 fixed point, positive orientation
   uint16_t px0, py0, px1, py1; // 8 : inclusive pixel bbox, clamped to the frame
   uint32_t uid;                // 4
-  uint32_t mat;                // 4 : material index
+  uint32_t atex;               // 4 : alpha-test texture, texel offset (kNoAlpha: none)
   float A[3], B[3], C[3];      // 36: e_k = A_k*x + B_k*y + C_k
   float invdet;                // 4
   float uv[6];                 // 24: only read for alpha-tested materials
-  uint32_t pad[2];             // 8
+  uint32_t atex_wh;            // 4 : alpha texture width | height << 16
+  uint32_t athr;               // 4 : alpha threshold (keep iff alpha > athr)
 };
 static_assert(sizeof(Rec) == 112, "Rec layout");
 
@@ -46,17 +50,18 @@ struct FrameDev {                // csg_frame mirror
   uint32_t frame_id;
 };
 
+// Geometry is stored de-indexed ("triangle soup"): the authored vertex and
+// index arrays are expanded at upload so a triangle is one contiguous 36-B
+// (positions) / 24-B (uvs) record.  World2 has ~2 vertices per triangle, so
+// the soup is the same size as the indexed arrays (12 B/vertex + 12 B/tri)
+// while removing the dependent index->vertex loads from k_setup and resolve.
 struct SceneDev {
-  const float* pos;
-  const uint32_t* tris;
-  const float* uvs;
-  const uint32_t* uv_tris;
-  const MeshDesc* meshes;
+  const float* tri_pos;        // [T][3][3] object space
+  const float* tri_uv;         // [T][3][2] (zeros for meshes without uvs)
+  const InstDesc* inst;        // [I]
   const MatDesc* mats;
   const TexDesc* texd;
   const uint8_t* texels;
-  const uint32_t* inst_mesh;
-  const int32_t* inst_label;
   uint32_t n_inst;
   float ambient[3], sun[3], sun_dir[3];
   uint32_t sky;                // packed r | g<<8 | b<<16
@@ -78,7 +83,7 @@ struct BatchDev {
   uint32_t* tile_fill;         // [F][n_tiles]
   uint32_t* bins;              // [F][bin_cap]
   uint32_t bin_cap;
-  uint32_t* overflow;          // [1] bit0 rec, bit1 bins
+  uint32_t* overflow;          // [16]: [0] bit0 rec, bit1 bins; [1..] profiling counters (CSG_DEBUG 512)
   // outputs (device)
   uint8_t* rgb;                // [F][H][W][3] or null
   int32_t* inst;               // [F][H][W] or null

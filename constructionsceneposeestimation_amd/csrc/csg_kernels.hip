@@ -32,7 +32,6 @@ namespace csg {
 
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr float kGuardPx = 1048576.0f;
-constexpr int kSmallRect = 8;    // tile rects up to this many tiles are counted per lane
 
 // ---------------------------------------------------------------------------
 // shared arithmetic (mirrors csg_oracle.c line by line)
@@ -88,32 +87,50 @@ __device__ __forceinline__ void interp_uv(const float* e, float ssum, const floa
   v = (l0 * uv[1] + l1 * uv[3]) + l2 * uv[5];
 }
 
-// Bilinear RGBA8, repeat wrap, 8-bit fixed weights. `only_alpha` skips RGB.
-__device__ __forceinline__ void tex_sample(const SceneDev& s, int tid, float u, float v, int out[4]) {
-  const TexDesc t = s.texd[tid];
-  const int tw = (int)t.width, th = (int)t.height;
+// Bilinear RGBA8, repeat wrap, 8-bit fixed weights (v flipped: row 0 = top).
+struct TexTap { uint32_t i00, i10, i01, i11; int wx, wy; };
+
+__device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {
   float tu = u * (float)tw - 0.5f;
   float tv = (1.0f - v) * (float)th - 0.5f;
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
-  const int wx = (int)((tu - fu) * 256.0f), wy = (int)((tv - fv) * 256.0f);
+  TexTap t;
+  t.wx = (int)((tu - fu) * 256.0f);
+  t.wy = (int)((tv - fv) * 256.0f);
   int x0 = (int)fu % tw;
   if (x0 < 0) x0 += tw;
   int y0 = (int)fv % th;
   if (y0 < 0) y0 += th;
   const int x1 = (x0 + 1 == tw) ? 0 : x0 + 1;
   const int y1 = (y0 + 1 == th) ? 0 : y0 + 1;
+  t.i00 = (uint32_t)(y0 * tw + x0); t.i10 = (uint32_t)(y0 * tw + x1);
+  t.i01 = (uint32_t)(y1 * tw + x0); t.i11 = (uint32_t)(y1 * tw + x1);
+  return t;
+}
+
+__device__ __forceinline__ int tex_channel(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, int sh, int wx,
+                                           int wy) {
+  const int top = (int)((c00 >> sh) & 255u) * (256 - wx) + (int)((c10 >> sh) & 255u) * wx;
+  const int bot = (int)((c01 >> sh) & 255u) * (256 - wx) + (int)((c11 >> sh) & 255u) * wx;
+  return (top * (256 - wy) + bot * wy + 32768) >> 16;
+}
+
+__device__ __forceinline__ void tex_sample(const SceneDev& s, int tid, float u, float v, int out[4]) {
+  const TexDesc t = s.texd[tid];
+  const TexTap k = tex_taps((int)t.width, (int)t.height, u, v);
   const uint32_t* base = reinterpret_cast<const uint32_t*>(s.texels) + t.offset;
-  const uint32_t c00 = base[(size_t)y0 * tw + x0], c10 = base[(size_t)y0 * tw + x1];
-  const uint32_t c01 = base[(size_t)y1 * tw + x0], c11 = base[(size_t)y1 * tw + x1];
+  const uint32_t c00 = base[k.i00], c10 = base[k.i10], c01 = base[k.i01], c11 = base[k.i11];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int sh = 8 * c;
-    const int top = (int)((c00 >> sh) & 255u) * (256 - wx) + (int)((c10 >> sh) & 255u) * wx;
-    const int bot = (int)((c01 >> sh) & 255u) * (256 - wx) + (int)((c11 >> sh) & 255u) * wx;
-    out[c] = (top * (256 - wy) + bot * wy + 32768) >> 16;
-  }
+  for (int c = 0; c < 4; ++c) out[c] = tex_channel(c00, c10, c01, c11, 8 * c, k.wx, k.wy);
+}
+
+// Alpha channel only (the alpha test); `wh` = width | height << 16.
+__device__ __forceinline__ int tex_alpha(const uint8_t* texels, uint32_t offset, uint32_t wh, float u, float v) {
+  const TexTap k = tex_taps((int)(wh & 0xFFFFu), (int)(wh >> 16), u, v);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(texels) + offset;
+  return tex_channel(base[k.i00], base[k.i10], base[k.i01], base[k.i11], 24, k.wx, k.wy);
 }
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -121,13 +138,20 @@ __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); 
 // ---------------------------------------------------------------------------
 // wave / block helpers (wave64)
 // ---------------------------------------------------------------------------
+// Inclusive wave64 prefix sum with DPP (VALU-rate lane moves, no LDS):
+// Hillis-Steele inside each 16-lane row (row_shr 1,2,4,8), then
+// row_bcast:15 / row_bcast:31 carry row totals across rows (gfx9 family).
+template <int Ctrl, int RowMask, int BankMask>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t v) {
+  return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, BankMask, false);
+}
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t n = __shfl_up(v, d, 64);
-    if (lane >= d) v += n;
-  }
+  v = dpp_add<0x111, 0xf, 0xf>(v);   // row_shr:1
+  v = dpp_add<0x112, 0xf, 0xf>(v);   // row_shr:2
+  v = dpp_add<0x114, 0xf, 0xf>(v);   // row_shr:4
+  v = dpp_add<0x118, 0xf, 0xf>(v);   // row_shr:8
+  v = dpp_add<0x142, 0xa, 0xf>(v);   // row_bcast:15 -> rows 1, 3
+  v = dpp_add<0x143, 0xc, 0xf>(v);   // row_bcast:31 -> rows 2, 3
   return v;
 }
 
@@ -147,38 +171,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   __syncthreads();
   total = tot;
   return off + inc - v;
-}
-
-// Order this wave's earlier LDS writes before its later LDS reads (cross-lane).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t n = __shfl_up(v, d, 64);
-    if (lane >= d) v = max(v, n);
-  }
-  return v;
-}
-
-// Owner lane of window item `lane` for ranges that start at window offset
-// `rel` (sorted by lane; `has` = the lane's range is non-empty).  `carry` is
-// the owner of the item just before the window and is updated in place.
-__device__ __forceinline__ uint32_t window_owner(uint32_t* mark, int lane, bool has, uint32_t rel, uint32_t& carry) {
-  mark[lane] = 0;
-  wave_lds_sync();
-  if (has && rel < 64u) mark[rel] = (uint32_t)lane + 1u;
-  wave_lds_sync();
-  const uint32_t m = wave_incl_max(mark[lane]);
-  const uint32_t own = m ? m - 1u : carry;
-  carry = __builtin_amdgcn_readlane(own, 63);
-  wave_lds_sync();
-  return own;
 }
 
 // last k in [0,256) with pre[k] <= j  (pre has 257 entries, j < pre[256])
@@ -319,13 +311,12 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     float c[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) c[k] = Cm[k];
-    const MeshDesc m = s.meshes[s.inst_mesh[i]];
-    const uint32_t* tri = s.tris + (size_t)(m.tbase + t) * 3;
+    const InstDesc m = s.inst[i];
+    const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
     Cv3 v[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const float* p = s.pos + (size_t)(m.vbase + tri[k]) * 3;
-      const float px = p[0], py = p[1], pz = p[2];
+      const float px = tp[3 * k], py = tp[3 * k + 1], pz = tp[3 * k + 2];
       v[k].x = dot4(c + 0, px, py, pz);
       v[k].y = dot4(c + 4, px, py, pz);
       v[k].w = dot4(c + 8, px, py, pz);
@@ -349,13 +340,16 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
         const MatDesc mat = s.mats[m.material];
         float uv[6] = {0, 0, 0, 0, 0, 0};
         if (mat.alpha_test && m.has_uv) {
-          const uint32_t* ut = s.uv_tris + (size_t)(m.tbase + t) * 3;
+          const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
 #pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            const float* q = s.uvs + (size_t)(m.uvbase + ut[k]) * 2;
-            uv[2 * k] = q[0];
-            uv[2 * k + 1] = q[1];
-          }
+          for (int k = 0; k < 6; ++k) uv[k] = tu[k];
+        }
+        uint32_t atex = kNoAlpha, atex_wh = 0, athr = 0;
+        if (mat.alpha_test && mat.texture >= 0) {
+          const TexDesc td = s.texd[mat.texture];
+          atex = td.offset;
+          atex_wh = td.width | (td.height << 16);
+          athr = mat.alpha_threshold;
         }
         const uint32_t uid = (i << kUidShift) | t;
         // Sutherland-Hodgman against W >= near over edges v0->v1, v1->v2, v2->v0
@@ -399,13 +393,14 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
           Rec rr;
           if (make_rec(s, su, sv, rr)) {
             rr.uid = uid;
-            rr.mat = m.material;
+            rr.atex = atex;
+            rr.atex_wh = atex_wh;
+            rr.athr = athr;
 #pragma unroll
             for (int k = 0; k < 3; ++k) { rr.A[k] = h.A[k]; rr.B[k] = h.B[k]; rr.C[k] = h.C[k]; }
             rr.invdet = h.invdet;
 #pragma unroll
             for (int k = 0; k < 6; ++k) rr.uv[k] = uv[k];
-            rr.pad[0] = rr.pad[1] = 0;
             if (nrec == 0) r0 = rr; else r1 = rr;
             ++nrec;
           }
@@ -565,12 +560,32 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   }
 }
 
-// Conservative range [xl, xr] (tile-local, clamped to [x0, x1]) of pixels on row
-// `py` whose centres can pass the exact edge tests of R.  Each edge
-// E(cx) = c0 - dy*cx is solved for its boundary in float relative to the tile
-// origin (|error| << 1/16 px for any boundary that lands inside the tile);
-// a 1/16-px margin keeps the range a superset of the exact set, and the
-// per-pixel integer test decides coverage, so results never depend on it.
+// Exact coverage test of the spec (fixed-point edges, top-left rule) for the
+// pixel centre (px, py).
+__device__ __forceinline__ bool covers(const Rec& R, int px, int py) {
+  const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
+  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+  bool inside = true;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
+    const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
+    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+    const int64_t ev = (int64_t)dx * (cy - ay) - (int64_t)dy * (cx - ax);
+    inside &= (ev + bias) >= 0;
+  }
+  return inside;
+}
+
+// Exact range [xl, xr] (tile-local, clamped to [x0, x1]) of the pixels on row
+// `py` whose centres R covers.  Each edge E(cx) = c0 - dy*cx is first solved
+// for its boundary in float relative to the tile origin (|error| << 1/16 px
+// for any boundary that lands inside the tile); a 1/16-px margin makes that
+// range a superset of the covered pixels, larger by at most one pixel per
+// side.  The covered set of a row is an interval (intersection of
+// half-planes), so walking inward with the exact integer test until a covered
+// pixel is found gives the exact range, and level-2 fragments skip the test.
+// (Measured: cheaper than pulling each edge's boundary back separately.)
 __device__ __forceinline__ void row_span(const Rec& R, int ox, int py, int x0, int x1, int& xl, int& xr) {
   const int32_t cy = py * 256 + 128;
   const int32_t OX = ox * 256;
@@ -593,405 +608,169 @@ __device__ __forceinline__ void row_span(const Rec& R, int ox, int py, int x0, i
   const float h = fmaxf(fminf((hi - 128.0f) * (1.0f / 256.0f) + 0.0625f, (float)x1 + 1.0f), (float)x0 - 1.0f);
   xl = max((int)ceilf(l), x0);
   xr = min((int)floorf(h), x1);
+  while (xl <= xr && !covers(R, ox + xl, py)) ++xl;
+  while (xr >= xl && !covers(R, ox + xr, py)) --xr;
 }
 
 // ---------------------------------------------------------------------------
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
 struct RasterCtx {
-  const SceneDev* s;
+  const uint8_t* texels;
   unsigned long long* zb;
   int ox, oy;
   float inv_near, inv_far;
   uint32_t dbg;
 };
 
-// Exact per-pixel test of the spec for record R at pixel (ox+lx, oy+ly):
-// fixed-point edges with the top-left rule, homogeneous depth, depth range,
-// early-z against the LDS key, alpha test, then ds_min_u64.
+// One fragment of record R at tile pixel (lx, ly), already known to be
+// covered: homogeneous depth, depth range, early-z against the LDS key,
+// alpha test (texture described inline in the record), then ds_min_u64.
 __device__ __forceinline__ void fragment(const RasterCtx& c, const Rec& R, int lx, int ly) {
   const int px = c.ox + lx, py = c.oy + ly;
-  const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
-  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
-  bool inside = true;
-#pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
-    const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
-    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-    const int64_t ev = (int64_t)dx * (cy - ay) - (int64_t)dy * (cx - ax);
-    inside &= (ev + bias) >= 0;
-  }
-  if (!inside) return;
   float e[3], ssum, invw;
   hom_eval(R.A, R.B, R.C, R.invdet, px, py, e, ssum, invw);
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | R.uid;
   unsigned long long* z = &c.zb[ly * kTile + lx];
   if (!(c.dbg & 16u) && key >= *z) return;
-  const MatDesc mat = c.s->mats[R.mat];
-  if (!(c.dbg & 4u) && mat.alpha_test && mat.texture >= 0) {
+  if (!(c.dbg & 4u) && R.atex != kNoAlpha) {
     float u, v;
-    int cc[4];
     interp_uv(e, ssum, R.uv, u, v);
-    tex_sample(*c.s, mat.texture, u, v, cc);
-    if (!(cc[3] > (int)mat.alpha_threshold)) return;
+    if (!(tex_alpha(c.texels, R.atex, R.atex_wh, u, v) > (int)R.athr)) return;
   }
   atomicMin(z, key);
 }
 
+// Stage bin entry `idx` into `slot`; returns its row count inside the tile.
 __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t* bins, uint32_t idx, uint32_t end,
-                                                 uint32_t rec_cap, Rec* slot, int ox, int oy, uint32_t& rect) {
-  uint32_t rows = 0;
-  rect = 0;
+                                                 uint32_t rec_cap, Rec* slot, int ox, int oy, uint32_t& row0) {
+  row0 = 0;
   const uint32_t r = (idx < end) ? bins[idx] : 0xFFFFFFFFu;
-  if (r < rec_cap) {
-    const uint4* src = reinterpret_cast<const uint4*>(recs + r);
-    uint4* dst = reinterpret_cast<uint4*>(slot);
+  if (r >= rec_cap) return 0;
+  const uint4* src = reinterpret_cast<const uint4*>(recs + r);
+  uint4* dst = reinterpret_cast<uint4*>(slot);
+  uint4 q[7];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) dst[k] = src[k];
-    const Rec& R = *slot;
-    const int x0 = max((int)R.px0, ox) - ox, x1 = min((int)R.px1, ox + kTile - 1) - ox;
-    const int y0 = max((int)R.py0, oy) - oy, y1 = min((int)R.py1, oy + kTile - 1) - oy;
-    if (x0 <= x1 && y0 <= y1) {
-      rows = (uint32_t)(y1 - y0 + 1);
-      rect = (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)x1 << 16);
+  for (int k = 0; k < 7; ++k) q[k] = src[k];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) dst[k] = q[k];
+  const uint32_t p0 = q[1].z, p1 = q[1].w;            // px0 | py0 << 16, px1 | py1 << 16
+  int y0 = max((int)(p0 >> 16), oy), y1 = min((int)(p1 >> 16), oy + kTile - 1);
+  const int x0 = max((int)(p0 & 0xFFFFu), ox), x1 = min((int)(p1 & 0xFFFFu), ox + kTile - 1);
+  if (x0 > x1 || y0 > y1) return 0u;
+  // Rows of the triangle inside this tile's column strip: the y-range of the
+  // triangle clipped to the pixel-centre lines x0..x1, in float relative to
+  // the tile, widened by half a pixel (>> any rounding here); the exact row
+  // spans of level 1 decide coverage, this only drops rows that cannot have any.
+  const int32_t X[3] = {(int32_t)q[0].x, (int32_t)q[0].y, (int32_t)q[0].z};
+  const int32_t Y[3] = {(int32_t)q[0].w, (int32_t)q[1].x, (int32_t)q[1].y};
+  const float sl = (float)(x0 * 256 + 128), sr = (float)(x1 * 256 + 128);
+  float fx[3], fy[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { fx[k] = (float)X[k]; fy[k] = (float)(Y[k] - oy * 256); }
+  float ylo = 1.0e30f, yhi = -1.0e30f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (fx[k] >= sl && fx[k] <= sr) { ylo = fminf(ylo, fy[k]); yhi = fmaxf(yhi, fy[k]); }
+    const int n = (k + 1) % 3;
+    const float dxe = fx[n] - fx[k], dye = fy[n] - fy[k];
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const float xs = side ? sr : sl;
+      if ((fx[k] - xs) * (fx[n] - xs) < 0.0f) {
+        const float yc = fy[k] + (xs - fx[k]) / dxe * dye;
+        ylo = fminf(ylo, yc);
+        yhi = fmaxf(yhi, yc);
+      }
     }
   }
-  return rows;
+  if (!(ylo <= yhi)) return 0u;
+  const int r0 = (int)ceilf((ylo - 128.0f - 128.0f) * (1.0f / 256.0f));
+  const int r1 = (int)floorf((yhi - 128.0f + 128.0f) * (1.0f / 256.0f));
+  y0 = max(y0, oy + r0);
+  y1 = min(y1, oy + r1);
+  row0 = (uint32_t)(y0 - oy);
+  return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
 
-struct RasterLds {
-  Rec lrec[kBlock];                 // 28 KiB staged bin records
-  uint32_t lrect[kBlock];
-  uint32_t pre[kBlock + 1];
-  uint32_t span[kBlock];
-  uint32_t pre2[kBlock + 1];
-  uint32_t wsum[kBlock / 64];
-};
-
-// V0/V2: block-level two-level expansion of 256-record batches.
-//   level 1: (record, row) items, one per thread -> conservative row span
-//   level 2: (span, pixel) items.  V0 finds each item's span by binary search;
-//            V2 gives every thread a contiguous run of items, searches once
-//            and walks (owner changes every ~3 items), keeping the record in
-//            registers while the owner's record is unchanged.
 template <int V>
-__device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds& L, uint32_t beg,
+struct RasterLds {
+  Rec lrec[kBlock];                     // 28 KiB staged bin records
+  uint32_t pre[kBlock + 1];             // row-item prefix per record
+  uint8_t row0[kBlock];                 // first tile row of each staged record
+  uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
+  uint32_t pre2[kBlock + 1];            // pixel-item prefix per span
+  uint32_t wsum[kBlock / 64];
+  uint8_t owner[V == 1 ? kBlock * kTile : 4];   // V1: span of every pixel item
+};
+static_assert(sizeof(RasterLds<0>) + kTilePix * 8 <= 40960, "k_raster<0> LDS must allow 4 workgroups per CU");
+
+// Block-level two-level expansion of 256-record batches.
+//   level 1: (record, row) items, one per thread -> exact row span
+//   level 2: (span, pixel) items; V0 finds each item's span by binary search
+//            over the span prefix, V1 reads it from a per-item owner map.
+template <int V>
+__device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds<V>& L, uint32_t beg,
                                              uint32_t end, const uint32_t* bins, const Rec* recs) {
   const int tid = threadIdx.x;
   for (uint32_t base = beg; base < end; base += kBlock) {
-    uint32_t rect;
-    const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, &L.lrec[tid], c.ox, c.oy, rect);
-    L.lrect[tid] = rect;
+    uint32_t row0;
+    const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, &L.lrec[tid], c.ox, c.oy, row0);
+    L.row0[tid] = (uint8_t)row0;
+    if ((b.dbg & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
+      atomicAdd(&b.overflow[1], 1u);
+      atomicAdd(&b.overflow[2], rows);
+    }
     uint32_t tot1;
     const uint32_t ex1 = block_excl_scan(rows, L.wsum, tot1);
     L.pre[tid] = ex1;
     if (tid == kBlock - 1) L.pre[kBlock] = ex1 + rows;
     __syncthreads();
-    for (uint32_t c1 = 0; c1 < tot1; c1 += kBlock) {
+    for (uint32_t c1 = 0; c1 < ((b.dbg & 256u) ? 0u : tot1); c1 += kBlock) {
       const uint32_t j1 = c1 + tid;
-      uint32_t w2 = 0;
+      uint32_t w2 = 0, sp = 0;
+      int xl = 0;
       if (j1 < tot1) {
         const int k = find_item(L.pre, j1);
-        const uint32_t rc = L.lrect[k];
-        const int ly = (int)((rc >> 8) & 255u) + (int)(j1 - L.pre[k]);
-        int xl, xr;
-        row_span(L.lrec[k], c.ox, c.oy + ly, (int)(rc & 255u), (int)((rc >> 16) & 255u), xl, xr);
+        const Rec& R = L.lrec[k];
+        const int x0 = max((int)R.px0 - c.ox, 0), x1 = min((int)R.px1 - c.ox, kTile - 1);
+        const int ly = (int)L.row0[k] + (int)(j1 - L.pre[k]);
+        int xr;
+        row_span(R, c.ox, c.oy + ly, x0, x1, xl, xr);
         if (xl <= xr) {
           w2 = (uint32_t)(xr - xl + 1);
-          L.span[tid] = (uint32_t)k | ((uint32_t)ly << 8) | ((uint32_t)xl << 16);
+          sp = (uint32_t)k | ((uint32_t)ly << 8);
         }
+      }
+      if ((b.dbg & 512u) && w2) {      // non-empty spans, level-2 items
+        atomicAdd(&b.overflow[3], 1u);
+        atomicAdd(&b.overflow[4], w2);
       }
       uint32_t tot2;
       const uint32_t ex2 = block_excl_scan(w2, L.wsum, tot2);
-      L.pre2[tid] = ex2;
-      if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
-      __syncthreads();
-      if constexpr (V == 0) {
-        for (uint32_t j = tid; j < ((b.dbg & 8u) ? 0u : tot2); j += kBlock) {
-          const int s2 = find_item(L.pre2, j);
-          const uint32_t sp = L.span[s2];
-          const int ly = (int)((sp >> 8) & 255u), lx = (int)((sp >> 16) & 255u) + (int)(j - L.pre2[s2]);
-          fragment(c, L.lrec[sp & 255u], lx, ly);
-        }
+      L.span[tid] = sp | ((ex2 - (uint32_t)xl + 32u) << 16);
+      if constexpr (V == 1) {
+        for (uint32_t q = 0; q < w2; ++q) L.owner[ex2 + q] = (uint8_t)tid;
       } else {
-        const uint32_t per = (tot2 + kBlock - 1) / kBlock;
-        uint32_t j = (uint32_t)tid * per;
-        const uint32_t jend = min(j + per, tot2);
-        if (j < jend) {
-          int s2 = find_item(L.pre2, j);
-          uint32_t sst = L.pre2[s2], snx = L.pre2[s2 + 1], sp = L.span[s2];
-          uint32_t k = sp & 255u;
-          Rec R = L.lrec[k];
-          for (; j < jend; ++j) {
-            while (j >= snx) {
-              ++s2;
-              sst = snx;
-              snx = L.pre2[s2 + 1];
-              sp = L.span[s2];
-              if ((sp & 255u) != k) {
-                k = sp & 255u;
-                R = L.lrec[k];
-              }
-            }
-            fragment(c, R, (int)((sp >> 16) & 255u) + (int)(j - sst), (int)((sp >> 8) & 255u));
-          }
-        }
+        L.pre2[tid] = ex2;
+        if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
       }
       __syncthreads();
-    }
-  }
-}
-
-struct WaveLds {
-  Rec lrec[kBlock];
-  uint32_t wmark[kBlock];
-};
-
-// V1: wave-level expansion (each wave owns 64 of every 256 records; owners
-// found by start marks + wave max-scan; no block barrier inside the loop).
-__device__ __forceinline__ void raster_wave(const RasterCtx& c, const BatchDev& b, WaveLds& L, uint32_t beg,
-                                            uint32_t end, const uint32_t* bins, const Rec* recs) {
-  const int tid = threadIdx.x;
-  const int wid = tid >> 6, lane = tid & 63;
-  Rec* wrec = &L.lrec[wid * 64];
-  uint32_t* mark = &L.wmark[wid * 64];
-  for (uint32_t base = beg + (uint32_t)wid * 64u; base < end; base += kBlock) {
-    uint32_t rect;
-    const uint32_t rows = stage_record(recs, bins, base + lane, end, b.rec_cap, &wrec[lane], c.ox, c.oy, rect);
-    wave_lds_sync();
-    const uint32_t inc1 = wave_incl_scan(rows);
-    const uint32_t st1 = inc1 - rows;
-    const uint32_t tot1 = __builtin_amdgcn_readlane(inc1, 63);
-    uint32_t carry1 = 0;
-    for (uint32_t w1 = 0; w1 < tot1; w1 += 64) {
-      const uint32_t own1 = window_owner(mark, lane, rows != 0, st1 - w1, carry1);
-      const uint32_t item1 = w1 + (uint32_t)lane;
-      const uint32_t o_st = __shfl(st1, (int)own1, 64), o_rect = __shfl(rect, (int)own1, 64);
-      uint32_t w2 = 0, sp = 0;
-      if (item1 < tot1) {
-        const int ly = (int)((o_rect >> 8) & 255u) + (int)(item1 - o_st);
-        int xl, xr;
-        row_span(wrec[own1], c.ox, c.oy + ly, (int)(o_rect & 255u), (int)((o_rect >> 16) & 255u), xl, xr);
-        if (xl <= xr) {
-          w2 = (uint32_t)(xr - xl + 1);
-          sp = own1 | ((uint32_t)ly << 8) | ((uint32_t)xl << 16);
-        }
+      for (uint32_t j = tid; j < ((b.dbg & 8u) ? 0u : tot2); j += kBlock) {
+        int s2;
+        if constexpr (V == 1) s2 = L.owner[j];
+        else s2 = find_item(L.pre2, j);
+        const uint32_t spj = L.span[s2];
+        fragment(c, L.lrec[spj & 255u], (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
-      const uint32_t inc2 = wave_incl_scan(w2);
-      const uint32_t st2 = inc2 - w2;
-      const uint32_t tot2 = __builtin_amdgcn_readlane(inc2, 63);
-      uint32_t carry2 = 0;
-      for (uint32_t w2b = 0; w2b < tot2; w2b += 64) {
-        const uint32_t own2 = window_owner(mark, lane, w2 != 0, st2 - w2b, carry2);
-        const uint32_t j = w2b + (uint32_t)lane;
-        const uint32_t o_sp = __shfl(sp, (int)own2, 64), o_st2 = __shfl(st2, (int)own2, 64);
-        if (j < tot2)
-          fragment(c, wrec[o_sp & 255u], (int)((o_sp >> 16) & 255u) + (int)(j - o_st2), (int)((o_sp >> 8) & 255u));
-      }
-    }
-    wave_lds_sync();
-  }
-}
-
-template <int V>
-__global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
-  __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
-  __shared__ typename std::conditional<V == 1, WaveLds, RasterLds>::type L;
-  __shared__ uint32_t lstat[5][kMaxLdsLabels];
-  const int tid = threadIdx.x;
-  const uint32_t tile = blockIdx.x, f = blockIdx.y;
-  const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
-  for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
-  const uint32_t nl = min(b.n_labels, (uint32_t)kMaxLdsLabels);
-  for (uint32_t l = tid; l < nl; l += kBlock) {
-    lstat[0][l] = 0; lstat[1][l] = 0xFFFFFFFFu; lstat[2][l] = 0xFFFFFFFFu; lstat[3][l] = 0; lstat[4][l] = 0;
-  }
-  const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
-  const uint32_t beg = min(toff[tile], b.bin_cap);
-  const uint32_t end = (b.dbg & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
-  const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
-  const Rec* recs = b.recs + (size_t)f * b.rec_cap;
-  RasterCtx c{&s, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg};
-  __syncthreads();
-  if constexpr (V == 1) raster_wave(c, b, L, beg, end, bins, recs);
-  else raster_block<V>(c, b, L, beg, end, bins, recs);
-  __syncthreads();
-
-  if (b.dbg & 1u) {   // ablation: keep the raster loop alive, skip the resolve
-    __syncthreads();
-    if (tid == 0 && zb[0] == 0ull && b.inst) b.inst[0] = 0;
-    return;
-  }
-  // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads
-  const int ly = tid >> 3, lx0 = (tid & 7) * 4;
-  const int py = oy + ly;
-  const size_t npx = (size_t)s.W * s.H;
-  if (py < (int)s.H) {
-    uint8_t rgb[12];
-    int32_t ids[4];
-    float dep[4];
-    uint32_t last_uid = 0xFFFFFFFFu;
-    // cached per-triangle state
-    Hom h;
-    float uvv[6];
-    int32_t label = -1;
-    int alb_const[3] = {0, 0, 0};
-    int tex = -1;
-    uint8_t mbase[3] = {0, 0, 0};
-    int q[3] = {0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int px = ox + lx0 + k;
-      const unsigned long long key = zb[ly * kTile + lx0 + k];
-      if (key == kEmptyKey || px >= (int)s.W) {
-        rgb[3 * k + 0] = (uint8_t)(s.sky & 255u);
-        rgb[3 * k + 1] = (uint8_t)((s.sky >> 8) & 255u);
-        rgb[3 * k + 2] = (uint8_t)((s.sky >> 16) & 255u);
-        ids[k] = -1;
-        dep[k] = INFINITY;
-        continue;
-      }
-      const uint32_t uid = (uint32_t)key;
-      const uint32_t i = uid >> kUidShift, t = uid & (kMaxTrisPerMesh - 1u);
-      if (uid != last_uid) {
-        last_uid = uid;
-        const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
-        float c[12];
-#pragma unroll
-        for (int z = 0; z < 12; ++z) c[z] = Cm[z];
-        const MeshDesc m = s.meshes[s.inst_mesh[i]];
-        const uint32_t* tri = s.tris + (size_t)(m.tbase + t) * 3;
-        float pobj[3][3];
-        Cv3 v[3];
-#pragma unroll
-        for (int z = 0; z < 3; ++z) {
-          const float* p = s.pos + (size_t)(m.vbase + tri[z]) * 3;
-          pobj[z][0] = p[0]; pobj[z][1] = p[1]; pobj[z][2] = p[2];
-          v[z].x = dot4(c + 0, p[0], p[1], p[2]);
-          v[z].y = dot4(c + 4, p[0], p[1], p[2]);
-          v[z].w = dot4(c + 8, p[0], p[1], p[2]);
-        }
-        hom_setup(v, h);
-        label = s.inst_label[i];
-        const MatDesc mat = s.mats[m.material];
-        tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
-        mbase[0] = mat.base[0]; mbase[1] = mat.base[1]; mbase[2] = mat.base[2];
-        if (tex >= 0) {
-          const uint32_t* ut = s.uv_tris + (size_t)(m.tbase + t) * 3;
-#pragma unroll
-          for (int z = 0; z < 3; ++z) {
-            const float* uq = s.uvs + (size_t)(m.uvbase + ut[z]) * 2;
-            uvv[2 * z] = uq[0];
-            uvv[2 * z + 1] = uq[1];
-          }
-        } else {
-          alb_const[0] = mbase[0]; alb_const[1] = mbase[1]; alb_const[2] = mbase[2];
-        }
-        // flat two-sided Lambert from the world-space face normal
-        const float* M = b.models + ((size_t)b.frames[f].xform_set * s.n_inst + i) * 16;
-        float mm[12];
-#pragma unroll
-        for (int z = 0; z < 12; ++z) mm[z] = M[z];
-        float pw[3][3];
-#pragma unroll
-        for (int z = 0; z < 3; ++z) {
-          pw[z][0] = dot4(mm + 0, pobj[z][0], pobj[z][1], pobj[z][2]);
-          pw[z][1] = dot4(mm + 4, pobj[z][0], pobj[z][1], pobj[z][2]);
-          pw[z][2] = dot4(mm + 8, pobj[z][0], pobj[z][1], pobj[z][2]);
-        }
-        const float e1x = pw[1][0] - pw[0][0], e1y = pw[1][1] - pw[0][1], e1z = pw[1][2] - pw[0][2];
-        const float e2x = pw[2][0] - pw[0][0], e2y = pw[2][1] - pw[0][1], e2z = pw[2][2] - pw[0][2];
-        const float nx = e1y * e2z - e1z * e2y;
-        const float ny = e1z * e2x - e1x * e2z;
-        const float nz = e1x * e2y - e1y * e2x;
-        const float nn = (nx * nx + ny * ny) + nz * nz;
-        float cs = 0.0f;
-        if (nn > 0.0f) {
-          const float d = (nx * s.sun_dir[0] + ny * s.sun_dir[1]) + nz * s.sun_dir[2];
-          cs = fabsf(d / sqrtf(nn));
-        }
-#pragma unroll
-        for (int z = 0; z < 3; ++z) {
-          const float shade = s.ambient[z] + s.sun[z] * cs;
-          int qq = (int)(shade * 256.0f + 0.5f);
-          q[z] = min(max(qq, 0), 65535);
-        }
-      }
-      float e[3], ssum, invw;
-      hom_eval(h.A, h.B, h.C, h.invdet, px, py, e, ssum, invw);
-      dep[k] = 1.0f / invw;
-      ids[k] = label;
-      int alb[3];
-      if (tex >= 0) {
-        float u, v;
-        int c[4];
-        interp_uv(e, ssum, uvv, u, v);
-        tex_sample(s, tex, u, v, c);
-#pragma unroll
-        for (int z = 0; z < 3; ++z) alb[z] = (c[z] * mbase[z] + 127) / 255;
-      } else {
-#pragma unroll
-        for (int z = 0; z < 3; ++z) alb[z] = alb_const[z];
-      }
-#pragma unroll
-      for (int z = 0; z < 3; ++z) {
-        const int o = (alb[z] * q[z] + 128) >> 8;
-        rgb[3 * k + z] = (uint8_t)min(o, 255);
-      }
-      if (label >= 0 && (uint32_t)label < nl) {
-        atomicAdd(&lstat[0][label], 1u);
-        atomicMin(&lstat[1][label], (uint32_t)px);
-        atomicMin(&lstat[2][label], (uint32_t)py);
-        atomicMax(&lstat[3][label], (uint32_t)px);
-        atomicMax(&lstat[4][label], (uint32_t)py);
-      }
-    }
-    const int px0 = ox + lx0;
-    const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
-    if (px0 + 3 < (int)s.W) {
-      if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(ids[0], ids[1], ids[2], ids[3]);
-      if (b.depth) *reinterpret_cast<float4*>(b.depth + o) = make_float4(dep[0], dep[1], dep[2], dep[3]);
-      if (b.rgb) {
-        uint32_t w3[3];
-#pragma unroll
-        for (int z = 0; z < 3; ++z)
-          w3[z] = (uint32_t)rgb[4 * z] | ((uint32_t)rgb[4 * z + 1] << 8) | ((uint32_t)rgb[4 * z + 2] << 16) |
-                  ((uint32_t)rgb[4 * z + 3] << 24);
-        uint32_t* d = reinterpret_cast<uint32_t*>(b.rgb + o * 3);
-        d[0] = w3[0]; d[1] = w3[1]; d[2] = w3[2];
-      }
-    } else {
-      for (int k = 0; k < 4 && px0 + k < (int)s.W; ++k) {
-        if (b.inst) b.inst[o + k] = ids[k];
-        if (b.depth) b.depth[o + k] = dep[k];
-        if (b.rgb) {
-          b.rgb[(o + k) * 3 + 0] = rgb[3 * k];
-          b.rgb[(o + k) * 3 + 1] = rgb[3 * k + 1];
-          b.rgb[(o + k) * 3 + 2] = rgb[3 * k + 2];
-        }
-      }
-    }
-  }
-  if (b.stats) {
-    __syncthreads();
-    uint32_t* st = b.stats + (size_t)f * b.n_labels * 5;
-    for (uint32_t l = tid; l < nl; l += kBlock) {
-      const uint32_t c = lstat[0][l];
-      if (c) {
-        atomicAdd(&st[l * 5 + 0], c);
-        atomicMin(&st[l * 5 + 1], lstat[1][l]);
-        atomicMin(&st[l * 5 + 2], lstat[2][l]);
-        atomicMax(&st[l * 5 + 3], lstat[3][l]);
-        atomicMax(&st[l * 5 + 4], lstat[4][l]);
-      }
+      __syncthreads();
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// per-pixel resolve (shared by the raster kernels)
+// per-pixel resolve
 // ---------------------------------------------------------------------------
 struct ResolveCache {
   uint32_t uid = 0xFFFFFFFFu;
@@ -1023,32 +802,29 @@ __device__ __forceinline__ void resolve_pixel(const SceneDev& s, const BatchDev&
     float c[12];
 #pragma unroll
     for (int z = 0; z < 12; ++z) c[z] = Cm[z];
-    const MeshDesc m = s.meshes[s.inst_mesh[i]];
-    const uint32_t* tri = s.tris + (size_t)(m.tbase + t) * 3;
+    const InstDesc m = s.inst[i];
+    const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
     float pobj[3][3];
     Cv3 v[3];
 #pragma unroll
     for (int z = 0; z < 3; ++z) {
-      const float* p = s.pos + (size_t)(m.vbase + tri[z]) * 3;
+      const float* p = tp + 3 * z;
       pobj[z][0] = p[0]; pobj[z][1] = p[1]; pobj[z][2] = p[2];
       v[z].x = dot4(c + 0, p[0], p[1], p[2]);
       v[z].y = dot4(c + 4, p[0], p[1], p[2]);
       v[z].w = dot4(c + 8, p[0], p[1], p[2]);
     }
     hom_setup(v, rc.h);
-    rc.label = s.inst_label[i];
+    rc.label = m.label;
     const MatDesc mat = s.mats[m.material];
     rc.tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
     rc.base[0] = mat.base[0]; rc.base[1] = mat.base[1]; rc.base[2] = mat.base[2];
     if (rc.tex >= 0) {
-      const uint32_t* ut = s.uv_tris + (size_t)(m.tbase + t) * 3;
+      const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
 #pragma unroll
-      for (int z = 0; z < 3; ++z) {
-        const float* uq = s.uvs + (size_t)(m.uvbase + ut[z]) * 2;
-        rc.uvv[2 * z] = uq[0];
-        rc.uvv[2 * z + 1] = uq[1];
-      }
+      for (int z = 0; z < 6; ++z) rc.uvv[z] = tu[z];
     }
+    // flat two-sided Lambert from the world-space face normal
     const float* M = b.models + ((size_t)b.frames[f].xform_set * s.n_inst + i) * 16;
     float mm[12];
 #pragma unroll
@@ -1100,152 +876,93 @@ __device__ __forceinline__ void resolve_pixel(const SceneDev& s, const BatchDev&
   rgb_out = o;
 }
 
-// ---------------------------------------------------------------------------
-// k_raster_px: pixel-parallel tile raster (V3).  One wave per 32x32 tile;
-// lane l owns pixel (l & 7, l >> 3) of each of the tile's sixteen 8x8 blocks
-// and keeps their (depth, uid) keys in registers.  The wave walks the tile's
-// bin; each record is read with wave-uniform (scalar) loads, its bbox picks
-// the blocks it can touch, one wave instruction stream tests 64 pixels of a
-// block at once, and a ballot skips blocks the triangle misses.  No LDS
-// z-buffer, no atomics, no scans, no barriers in the raster loop.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_raster_px(SceneDev s, BatchDev b) {
-  __shared__ uint32_t o_rgb[kTilePix];
-  __shared__ int32_t o_id[kTilePix];
-  __shared__ float o_dep[kTilePix];
-  const int lane = threadIdx.x;
+template <int V>
+__global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
+  __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
+  __shared__ union Lds {
+    RasterLds<V> r;                                  // raster loop
+    uint32_t lstat[5][kMaxLdsLabels];                // resolve: per-label pixel count + box
+  } L;
+  const int tid = threadIdx.x;
   const uint32_t tile = blockIdx.x, f = blockIdx.y;
   const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
-  const int lxo = lane & 7, lyo = lane >> 3;
+  for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
   const uint32_t beg = min(toff[tile], b.bin_cap);
   const uint32_t end = (b.dbg & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
-  const uint32_t* __restrict__ bins = b.bins + (size_t)f * b.bin_cap;
-  const Rec* __restrict__ recs = b.recs + (size_t)f * b.rec_cap;
-  const float inv_near = 1.0f / s.near_clip, inv_far = 1.0f / s.far_clip;
-  unsigned long long zk[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) zk[k] = kEmptyKey;
+  const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
+  const Rec* recs = b.recs + (size_t)f * b.rec_cap;
+  RasterCtx c{s.texels, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg};
+  __syncthreads();
+  raster_block<V>(c, b, L.r, beg, end, bins, recs);
+  __syncthreads();
 
-  for (uint32_t i = beg; i < end; ++i) {
-    const uint32_t ri = __builtin_amdgcn_readfirstlane(bins[i]);
-    if (ri >= b.rec_cap) continue;
-    const Rec& R = recs[ri];
-    const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
-    int32_t ax[3], ay[3], dx[3], dy[3], bias[3];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      ax[e] = R.x[ea[e]];
-      ay[e] = R.y[ea[e]];
-      dx[e] = R.x[eb[e]] - ax[e];
-      dy[e] = R.y[eb[e]] - ay[e];
-      bias[e] = (dy[e] < 0 || (dy[e] == 0 && dx[e] > 0)) ? 0 : -1;
-    }
-    const int bx0 = ((int)R.px0 - ox) >> 3, bx1 = ((int)R.px1 - ox) >> 3;
-    const int by0 = ((int)R.py0 - oy) >> 3, by1 = ((int)R.py1 - oy) >> 3;
-    const float A0 = R.A[0], A1 = R.A[1], A2 = R.A[2], B0 = R.B[0], B1 = R.B[1], B2 = R.B[2];
-    const float C0 = R.C[0], C1 = R.C[1], C2 = R.C[2], invdet = R.invdet;
-    const uint32_t uid = R.uid;
-    const MatDesc mat = s.mats[R.mat];
-    const bool alpha = mat.alpha_test && mat.texture >= 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int bx = k & 3, by = k >> 2;
-      if (bx < bx0 || bx > bx1 || by < by0 || by > by1) continue;       // uniform
-      const int px = ox + bx * 8 + lxo, py = oy + by * 8 + lyo;
-      const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
-      bool inside = px <= (int)R.px1 && py <= (int)R.py1 && px >= (int)R.px0 && py >= (int)R.py0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int64_t ev = (int64_t)dx[e] * (cy - ay[e]) - (int64_t)dy[e] * (cx - ax[e]);
-        inside &= (ev + bias[e]) >= 0;
-      }
-      if (__ballot(inside) == 0) continue;                              // wave-uniform skip
-      if (!inside) continue;
-      const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
-      const float e0 = (A0 * fx + B0 * fy) + C0;
-      const float e1 = (A1 * fx + B1 * fy) + C1;
-      const float e2 = (A2 * fx + B2 * fy) + C2;
-      const float ssum = (e0 + e1) + e2;
-      const float invw = ssum * invdet;
-      if (!(invw >= inv_far && invw <= inv_near)) continue;
-      const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | uid;
-      if (key >= zk[k]) continue;
-      if (alpha && !(b.dbg & 4u)) {
-        const float ee[3] = {e0, e1, e2};
-        float u, v;
-        int cc[4];
-        interp_uv(ee, ssum, R.uv, u, v);
-        tex_sample(s, mat.texture, u, v, cc);
-        if (!(cc[3] > (int)mat.alpha_threshold)) continue;
-      }
-      zk[k] = key;
-    }
-  }
-  if (b.dbg & 1u) {
-    uint64_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) acc ^= zk[k];
-    if (acc == 0x1234ull && b.inst) b.inst[0] = 0;
+  if (b.dbg & 1u) {   // ablation: keep the raster loop alive, skip the resolve
+    if (tid == 0 && zb[0] == 0ull && b.inst) b.inst[0] = 0;
     return;
   }
-  // resolve into LDS (tile-linear), then coalesced row stores
-  ResolveCache rc;
-  const uint32_t nl = b.stats ? b.n_labels : 0u;
-  uint32_t* stf = b.stats ? b.stats + (size_t)f * b.n_labels * 5 : nullptr;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int lx = (k & 3) * 8 + lxo, ly = (k >> 2) * 8 + lyo;
-    const int px = ox + lx, py = oy + ly;
-    uint32_t rgb = 0;
-    int32_t id = -1;
-    float dep = INFINITY;
-    if (px < (int)s.W && py < (int)s.H) {
-      resolve_pixel(s, b, f, px, py, zk[k], rc, rgb, id, dep);
-      if (id >= 0 && (uint32_t)id < nl) {
-        atomicAdd(&stf[id * 5 + 0], 1u);
-        atomicMin(&stf[id * 5 + 1], (uint32_t)px);
-        atomicMin(&stf[id * 5 + 2], (uint32_t)py);
-        atomicMax(&stf[id * 5 + 3], (uint32_t)px);
-        atomicMax(&stf[id * 5 + 4], (uint32_t)py);
-      }
-    }
-    o_rgb[ly * kTile + lx] = rgb;
-    o_id[ly * kTile + lx] = id;
-    o_dep[ly * kTile + lx] = dep;
+  const uint32_t nl = min(b.n_labels, (uint32_t)kMaxLdsLabels);
+  for (uint32_t l = tid; l < nl; l += kBlock) {
+    L.lstat[0][l] = 0; L.lstat[1][l] = 0xFFFFFFFFu; L.lstat[2][l] = 0xFFFFFFFFu; L.lstat[3][l] = 0; L.lstat[4][l] = 0;
   }
   __syncthreads();
+  // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads
+  const int ly = tid >> 3, lx0 = (tid & 7) * 4;
+  const int py = oy + ly;
   const size_t npx = (size_t)s.W * s.H;
-  // 32 rows x 32 px: each lane stores 4 consecutive pixels of a row per step
+  if (py < (int)s.H) {
+    uint32_t rgb[4];
+    int32_t ids[4];
+    float dep[4];
+    ResolveCache rc;
 #pragma unroll
-  for (int step = 0; step < 4; ++step) {
-    const int q = step * 64 + lane;          // 256 quads of 4 pixels
-    const int ly = q >> 3, lx = (q & 7) * 4;
-    const int py = oy + ly, px = ox + lx;
-    if (py >= (int)s.H) continue;
-    const size_t o = (size_t)f * npx + (size_t)py * s.W + px;
-    const int t = ly * kTile + lx;
-    if (px + 3 < (int)s.W) {
-      if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(o_id[t], o_id[t + 1], o_id[t + 2], o_id[t + 3]);
-      if (b.depth)
-        *reinterpret_cast<float4*>(b.depth + o) = make_float4(o_dep[t], o_dep[t + 1], o_dep[t + 2], o_dep[t + 3]);
+    for (int k = 0; k < 4; ++k) {
+      const int px = ox + lx0 + k;
+      const unsigned long long key = px < (int)s.W ? zb[ly * kTile + lx0 + k] : kEmptyKey;
+      resolve_pixel(s, b, f, px, py, key, rc, rgb[k], ids[k], dep[k]);
+      const int32_t label = ids[k];
+      if (label >= 0 && (uint32_t)label < nl) {
+        atomicAdd(&L.lstat[0][label], 1u);
+        atomicMin(&L.lstat[1][label], (uint32_t)px);
+        atomicMin(&L.lstat[2][label], (uint32_t)py);
+        atomicMax(&L.lstat[3][label], (uint32_t)px);
+        atomicMax(&L.lstat[4][label], (uint32_t)py);
+      }
+    }
+    const int px0 = ox + lx0;
+    const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
+    if (px0 + 3 < (int)s.W) {
+      if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(ids[0], ids[1], ids[2], ids[3]);
+      if (b.depth) *reinterpret_cast<float4*>(b.depth + o) = make_float4(dep[0], dep[1], dep[2], dep[3]);
       if (b.rgb) {
-        const uint32_t c0 = o_rgb[t], c1 = o_rgb[t + 1], c2 = o_rgb[t + 2], c3 = o_rgb[t + 3];
         uint32_t* d = reinterpret_cast<uint32_t*>(b.rgb + o * 3);
-        d[0] = c0 | (c1 << 24);
-        d[1] = (c1 >> 8) | (c2 << 16);
-        d[2] = (c2 >> 16) | (c3 << 8);
+        d[0] = rgb[0] | (rgb[1] << 24);
+        d[1] = (rgb[1] >> 8) | (rgb[2] << 16);
+        d[2] = (rgb[2] >> 16) | (rgb[3] << 8);
       }
     } else {
-      for (int k = 0; k < 4 && px + k < (int)s.W; ++k) {
-        if (b.inst) b.inst[o + k] = o_id[t + k];
-        if (b.depth) b.depth[o + k] = o_dep[t + k];
+      for (int k = 0; k < 4 && px0 + k < (int)s.W; ++k) {
+        if (b.inst) b.inst[o + k] = ids[k];
+        if (b.depth) b.depth[o + k] = dep[k];
         if (b.rgb) {
-          const uint32_t cpx = o_rgb[t + k];
-          b.rgb[(o + k) * 3 + 0] = (uint8_t)(cpx & 255u);
-          b.rgb[(o + k) * 3 + 1] = (uint8_t)((cpx >> 8) & 255u);
-          b.rgb[(o + k) * 3 + 2] = (uint8_t)((cpx >> 16) & 255u);
+          b.rgb[(o + k) * 3 + 0] = (uint8_t)(rgb[k] & 255u);
+          b.rgb[(o + k) * 3 + 1] = (uint8_t)((rgb[k] >> 8) & 255u);
+          b.rgb[(o + k) * 3 + 2] = (uint8_t)((rgb[k] >> 16) & 255u);
         }
+      }
+    }
+  }
+  if (b.stats) {
+    __syncthreads();
+    uint32_t* st = b.stats + (size_t)f * b.n_labels * 5;
+    for (uint32_t l = tid; l < nl; l += kBlock) {
+      const uint32_t cnt = L.lstat[0][l];
+      if (cnt) {
+        atomicAdd(&st[l * 5 + 0], cnt);
+        atomicMin(&st[l * 5 + 1], L.lstat[1][l]);
+        atomicMin(&st[l * 5 + 2], L.lstat[2][l]);
+        atomicMax(&st[l * 5 + 3], L.lstat[3][l]);
+        atomicMax(&st[l * 5 + 4], L.lstat[4][l]);
       }
     }
   }
@@ -1341,10 +1058,9 @@ void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st
 
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st, int variant) {
   dim3 g(s.n_tiles, F);
-  if (variant == 0) hipLaunchKernelGGL(k_raster<0>, g, dim3(kBlock), 0, st, s, b);
-  else if (variant == 1) hipLaunchKernelGGL(k_raster<1>, g, dim3(kBlock), 0, st, s, b);
-  else if (variant == 2) hipLaunchKernelGGL(k_raster<2>, g, dim3(kBlock), 0, st, s, b);
-  else hipLaunchKernelGGL(k_raster_px, g, dim3(64), 0, st, s, b);
+  // variant: 0 = production; 1 = owner-map level 2 (kept for A/B)
+  if (variant == 1) hipLaunchKernelGGL(k_raster<1>, g, dim3(kBlock), 0, st, s, b);
+  else hipLaunchKernelGGL(k_raster<0>, g, dim3(kBlock), 0, st, s, b);
 }
 
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st) {

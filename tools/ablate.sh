@@ -1,5 +1,5 @@
 #!/bin/bash
-# k_raster ablations (CSG_DEBUG bits): 1 no resolve, 2 no raster loop, 4 no alpha test,
+# k_raster ablations (CSG_DEBUG bits): 1 no resolve, 2 no raster loop, 4 no alpha test, 256 no level 1,
 # 8 no level-2 fragments, 16 no early-z read.  Same binary, one process per setting.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
