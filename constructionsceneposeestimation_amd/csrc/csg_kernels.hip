@@ -173,12 +173,16 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   return off + inc - v;
 }
 
-// last k in [0,256) with pre[k] <= j  (pre has 257 entries, j < pre[256])
+// last k in [0,256) with pre[k] <= j  (pre has 257 entries, nondecreasing,
+// pre[0] <= j < pre[256]).  4-ary search: each step issues three independent
+// LDS reads, so the dependent chain is 4 LDS round trips instead of 8.
 __device__ __forceinline__ int find_item(const uint32_t* pre, uint32_t j) {
   int lo = 0;
 #pragma unroll
-  for (int step = 128; step > 0; step >>= 1)
-    if (pre[lo + step] <= j) lo += step;
+  for (int step = 64; step > 0; step >>= 2) {
+    const uint32_t a = pre[lo + step], b = pre[lo + 2 * step], c = pre[lo + 3 * step];
+    lo += ((a <= j) + (b <= j) + (c <= j)) * step;
+  }
   return lo;
 }
 
@@ -560,47 +564,40 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   }
 }
 
-// Exact coverage test of the spec (fixed-point edges, top-left rule) for the
-// pixel centre (px, py).
-__device__ __forceinline__ bool covers(const Rec& R, int px, int py) {
-  const int32_t cx = px * 256 + 128, cy = py * 256 + 128;
-  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
-  bool inside = true;
-#pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
-    const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
-    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-    const int64_t ev = (int64_t)dx * (cy - ay) - (int64_t)dy * (cx - ax);
-    inside &= (ev + bias) >= 0;
-  }
-  return inside;
-}
-
 // Exact range [xl, xr] (tile-local, clamped to [x0, x1]) of the pixels on row
-// `py` whose centres R covers.  Each edge E(cx) = c0 - dy*cx is first solved
-// for its boundary in float relative to the tile origin (|error| << 1/16 px
-// for any boundary that lands inside the tile); a 1/16-px margin makes that
-// range a superset of the covered pixels, larger by at most one pixel per
-// side.  The covered set of a row is an interval (intersection of
-// half-planes), so walking inward with the exact integer test until a covered
-// pixel is found gives the exact range, and level-2 fragments skip the test.
-// (Measured: cheaper than pulling each edge's boundary back separately.)
-__device__ __forceinline__ void row_span(const Rec& R, int ox, int py, int x0, int x1, int& xl, int& xr) {
-  const int32_t cy = py * 256 + 128;
-  const int32_t OX = ox * 256;
+// `ly` whose centres R covers.  Per edge, in tile-relative fixed point,
+// E(lx) = c0 - dy*(256*lx + 128) with c0 = dx*(cy - ay) + dy*ax + bias exact
+// (the spec's edge function with the top-left bias).  The boundary of each
+// edge is solved in float (|error| << 1/16 px for a boundary near the tile);
+// a 1/16-px margin makes the float range a superset of the covered pixels,
+// larger by at most one pixel per side.  The covered set of a row is an
+// interval (intersection of half-planes), so walking inward with the exact
+// test until a covered pixel is found gives the exact range, and level-2
+// fragments skip the test.  `Small` records (every vertex within 64 px of the
+// tile origin) do the exact arithmetic in 32 bits with full-rate 24-bit
+// multiplies; others in int64.
+template <bool Small>
+__device__ __forceinline__ void row_span(const Rec& R, int ox, int oy, int ly, int x0, int x1, int& xl, int& xr,
+                                         bool no_exact) {
+  using T = typename std::conditional<Small, int32_t, int64_t>::type;
+  const int32_t OX = ox * 256, OY = oy * 256;
+  const int32_t cy = ly * 256 + 128;
+  T c0[3];
+  int32_t dys[3];
   float lo = -1.0e30f, hi = 1.0e30f;
   const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
-    const int32_t ax = R.x[ea[e]], ay = R.y[ea[e]];
-    const int32_t dx = R.x[eb[e]] - ax, dy = R.y[eb[e]] - ay;
+    const int32_t ax = R.x[ea[e]] - OX, ay = R.y[ea[e]] - OY;
+    const int32_t dx = R.x[eb[e]] - R.x[ea[e]], dy = R.y[eb[e]] - R.y[ea[e]];
     const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-    const int64_t c0 = (int64_t)dx * (cy - ay) + (int64_t)dy * (ax - OX) + bias;   // E = c0 - dy*(cx-OX)
+    if constexpr (Small) c0[e] = __mul24(dx, cy - ay) + __mul24(dy, ax) + bias;
+    else c0[e] = (int64_t)dx * (cy - ay) + (int64_t)dy * ax + bias;
+    dys[e] = dy;
     if (dy == 0) {
-      if (c0 < 0) hi = -1.0e30f;
+      if (c0[e] < 0) hi = -1.0e30f;
     } else {
-      const float t = __fdividef((float)c0, (float)dy);   // approximate: covered by the margin
+      const float t = __fdividef((float)c0[e], (float)dy);   // approximate: covered by the margin
       if (dy > 0) hi = fminf(hi, t); else lo = fmaxf(lo, t);
     }
   }
@@ -608,8 +605,23 @@ __device__ __forceinline__ void row_span(const Rec& R, int ox, int py, int x0, i
   const float h = fmaxf(fminf((hi - 128.0f) * (1.0f / 256.0f) + 0.0625f, (float)x1 + 1.0f), (float)x0 - 1.0f);
   xl = max((int)ceilf(l), x0);
   xr = min((int)floorf(h), x1);
-  while (xl <= xr && !covers(R, ox + xl, py)) ++xl;
-  while (xr >= xl && !covers(R, ox + xr, py)) --xr;
+  if (no_exact) return;   // ablation only (CSG_DEBUG 2048): superset span
+  auto covers = [&](int lx) {
+    const int32_t cx = lx * 256 + 128;
+    bool in = true;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      if constexpr (Small) in &= c0[e] - __mul24(dys[e], cx) >= 0;
+      else in &= c0[e] - (int64_t)dys[e] * cx >= 0;
+    }
+    return in;
+  };
+  // normally zero or one step: keep the loops scalar (the loop vectorizer
+  // otherwise evaluates eight speculative steps per trip)
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+  while (xl <= xr && !covers(xl)) ++xl;
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+  while (xr >= xl && !covers(xr)) --xr;
 }
 
 // ---------------------------------------------------------------------------
@@ -690,7 +702,11 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
   const int r1 = (int)floorf((yhi - 128.0f + 128.0f) * (1.0f / 256.0f));
   y0 = max(y0, oy + r0);
   y1 = min(y1, oy + r1);
-  row0 = (uint32_t)(y0 - oy);
+  bool small = true;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    small &= abs(X[k] - ox * 256) < (1 << 14) && abs(Y[k] - oy * 256) < (1 << 14);
+  row0 = (uint32_t)(y0 - oy) | (small ? 0x80u : 0u);
   return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
 
@@ -698,7 +714,7 @@ template <int V>
 struct RasterLds {
   Rec lrec[kBlock];                     // 28 KiB staged bin records
   uint32_t pre[kBlock + 1];             // row-item prefix per record
-  uint8_t row0[kBlock];                 // first tile row of each staged record
+  uint8_t row0[kBlock];                 // first tile row of each staged record | 0x80 if small
   uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
   uint32_t pre2[kBlock + 1];            // pixel-item prefix per span
   uint32_t wsum[kBlock / 64];
@@ -735,9 +751,12 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         const int k = find_item(L.pre, j1);
         const Rec& R = L.lrec[k];
         const int x0 = max((int)R.px0 - c.ox, 0), x1 = min((int)R.px1 - c.ox, kTile - 1);
-        const int ly = (int)L.row0[k] + (int)(j1 - L.pre[k]);
+        const uint32_t r0b = L.row0[k];
+        const int ly = (int)(r0b & 31u) + (int)(j1 - L.pre[k]);
         int xr;
-        row_span(R, c.ox, c.oy + ly, x0, x1, xl, xr);
+        if (b.dbg & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
+        else if (r0b & 0x80u) row_span<true>(R, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
+        else row_span<false>(R, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
         if (xl <= xr) {
           w2 = (uint32_t)(xr - xl + 1);
           sp = (uint32_t)k | ((uint32_t)ly << 8);
