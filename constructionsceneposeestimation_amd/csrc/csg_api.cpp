@@ -96,8 +96,9 @@ struct csg_ctx {
   // internal outputs (host-output mode / scratch)
   DevBuf<uint8_t> o_rgb;
   DevBuf<int32_t> o_inst;
-  DevBuf<float> o_depth, o_kp_uv;
+  DevBuf<float> o_depth, o_kp_uv, kp_w;
   DevBuf<int32_t> o_kp_vis;
+  DevBuf<uint32_t> kp_pix, kp_tiles;
   DevBuf<uint32_t> o_stats;
 
   // timing: ring of per-batch event quintuples (recorded, never waited on in the loop)
@@ -173,6 +174,7 @@ void csg_destroy(csg_ctx* c) {
   c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
   c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
+  c->kp_w.release(); c->kp_pix.release(); c->kp_tiles.release();
   if (c->h_frames) (void)hipHostFree(c->h_frames);
   for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
@@ -489,8 +491,14 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     }
   }
   if (!out->inst_stats) b.stats = nullptr;
+  b.tile_words = (c->n_tiles + 31u) / 32u;
   if (want_kp) {
-    if (!b.depth) { HIP_TRY(c, c->o_depth.alloc(F * npx)); b.depth = c->o_depth.p; }
+    HIP_TRY(c, c->kp_w.alloc((size_t)F * c->n_kp));
+    HIP_TRY(c, c->kp_pix.alloc((size_t)F * c->n_kp));
+    HIP_TRY(c, c->kp_tiles.alloc((size_t)F * b.tile_words));
+    b.kp_w = c->kp_w.p;
+    b.kp_pix = c->kp_pix.p;
+    b.kp_tiles = c->kp_tiles.p;
     if (!b.kp_uv) { HIP_TRY(c, c->o_kp_uv.alloc((size_t)F * c->n_kp * 2)); b.kp_uv = c->o_kp_uv.p; }
     if (!b.kp_vis) { HIP_TRY(c, c->o_kp_vis.alloc((size_t)F * c->n_kp)); b.kp_vis = c->o_kp_vis.p; }
   }
@@ -499,6 +507,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
   HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
   HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), st));
+  if (want_kp) HIP_TRY(c, hipMemsetAsync(b.kp_tiles, 0, sizeof(uint32_t) * F * b.tile_words, st));
   launch_init_stats(b, F, st);
   if (c->timing) {
     const uint32_t slot = (uint32_t)(c->ring_count % csg_ctx::kRing);
@@ -514,9 +523,9 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   launch_scan(s, b, F, st);
   launch_bin(s, b, F, st);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
-  launch_raster(s, b, F, st, c->raster_variant);
+  launch_keypoints(s, b, F, st);   // projection; k_raster depth-tests against its z-buffer
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
-  launch_keypoints(s, b, F, st);
+  launch_raster(s, b, F, st, c->raster_variant);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
   HIP_TRY(c, hipGetLastError());
   c->last_F = F;
@@ -597,8 +606,8 @@ int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
     HIP_TRY(c, hipEventElapsedTime(&e, c->ev[3], c->ev[4]));
     st->ms_setup = a;
     st->ms_bin = b;
-    st->ms_raster = d;
-    st->ms_keypoints = e;
+    st->ms_keypoints = d;
+    st->ms_raster = e;
     st->ms_total = a + b + d + e;
   }
   return CSG_OK;
@@ -625,8 +634,8 @@ int csg_timing_read(csg_ctx* c, csg_timing* out) {
     HIP_TRY(c, hipEventElapsedTime(&f, e[3], e[4]));
     out->ms_setup += a;
     out->ms_bin += b;
-    out->ms_raster += d;
-    out->ms_keypoints += f;
+    out->ms_keypoints += d;
+    out->ms_raster += f;
     out->frames += c->ring_frames[k];
   }
   out->batches = (uint32_t)n;

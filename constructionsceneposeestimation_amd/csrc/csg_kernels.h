@@ -94,6 +94,10 @@ struct BatchDev {
   uint32_t n_kp;
   float* kp_uv;                // [F][K][2]
   int32_t* kp_vis;             // [F][K]
+  float* kp_w;                 // [F][K] camera-space w (distance to the image plane)
+  uint32_t* kp_pix;            // [F][K] px | py << 16 of in-view keypoints, else ~0
+  uint32_t* kp_tiles;          // [F][tile_words] bitmap of tiles holding an in-view keypoint
+  uint32_t tile_words;
   uint32_t dbg;                // ablation switches for profiling only (CSG_DEBUG env; 0 in production)
 };
 

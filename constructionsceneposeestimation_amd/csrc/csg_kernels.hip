@@ -21,7 +21,8 @@
 //                                (depth,uid) z-buffer in LDS (ds_min_u64),
 //                                then resolve: texture, shade, instance id,
 //                                depth, coalesced HBM writes, label stats
-//   k_keypoints(K x F)           3D->2D projection + depth-tested visibility
+//   k_keypoints(K x F)           3D->2D keypoint projection (before k_raster;
+//                                k_raster depth-tests those in its tile)
 #include <math.h>
 
 #include <type_traits>
@@ -791,108 +792,128 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
 // ---------------------------------------------------------------------------
 // per-pixel resolve
 // ---------------------------------------------------------------------------
-struct ResolveCache {
-  uint32_t uid = 0xFFFFFFFFu;
-  Hom h;
-  float uvv[6];
-  int32_t label = -1;
-  int tex = -1;
-  int base[3] = {0, 0, 0};
-  int q[3] = {0, 0, 0};
+// Everything the resolve needs about one winning triangle (84 B).
+struct ShadeEntry {
+  float A[3], B[3], C[3], invdet;   // homogeneous edge coefficients of the original triangle
+  float uv[6];
+  int32_t label;
+  int32_t tex;                      // -1: flat albedo
+  uint32_t base;                    // albedo multiplier r | g << 8 | b << 16
+  uint32_t q01, q2;                 // shade factors (x256): q0 | q1 << 16, q2
 };
 
-// Shade one pixel from its winning (depth, uid) key: depth, instance id and
-// RGB exactly as csg_oracle.c's resolve (recomputes the triangle's clip
-// coordinates; cached across pixels of the same triangle).
-__device__ __forceinline__ void resolve_pixel(const SceneDev& s, const BatchDev& b, uint32_t f, int px, int py,
-                                              unsigned long long key, ResolveCache& rc, uint32_t& rgb_out,
-                                              int32_t& id_out, float& depth_out) {
-  if (key == kEmptyKey) {
-    rgb_out = s.sky & 0xFFFFFFu;
-    id_out = -1;
-    depth_out = INFINITY;
-    return;
-  }
-  const uint32_t uid = (uint32_t)key;
+// Triangle setup of the resolve, exactly as csg_oracle.c: clip coordinates,
+// homogeneous coefficients, material, uvs, flat two-sided Lambert from the
+// world-space face normal.
+__device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b, uint32_t f, uint32_t uid,
+                                            ShadeEntry& e) {
   const uint32_t i = uid >> kUidShift, t = uid & (kMaxTrisPerMesh - 1u);
-  if (uid != rc.uid) {
-    rc.uid = uid;
-    const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
-    float c[12];
+  const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
+  const float* M = b.models + ((size_t)b.frames[f].xform_set * s.n_inst + i) * 16;
+  const InstDesc m = s.inst[i];
+  float c[12], mm[12];
 #pragma unroll
-    for (int z = 0; z < 12; ++z) c[z] = Cm[z];
-    const InstDesc m = s.inst[i];
-    const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
-    float pobj[3][3];
-    Cv3 v[3];
+  for (int z = 0; z < 12; ++z) { c[z] = Cm[z]; mm[z] = M[z]; }
+  const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
+  float pobj[3][3];
+  Cv3 v[3];
 #pragma unroll
-    for (int z = 0; z < 3; ++z) {
-      const float* p = tp + 3 * z;
-      pobj[z][0] = p[0]; pobj[z][1] = p[1]; pobj[z][2] = p[2];
-      v[z].x = dot4(c + 0, p[0], p[1], p[2]);
-      v[z].y = dot4(c + 4, p[0], p[1], p[2]);
-      v[z].w = dot4(c + 8, p[0], p[1], p[2]);
-    }
-    hom_setup(v, rc.h);
-    rc.label = m.label;
-    const MatDesc mat = s.mats[m.material];
-    rc.tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
-    rc.base[0] = mat.base[0]; rc.base[1] = mat.base[1]; rc.base[2] = mat.base[2];
-    if (rc.tex >= 0) {
-      const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
-#pragma unroll
-      for (int z = 0; z < 6; ++z) rc.uvv[z] = tu[z];
-    }
-    // flat two-sided Lambert from the world-space face normal
-    const float* M = b.models + ((size_t)b.frames[f].xform_set * s.n_inst + i) * 16;
-    float mm[12];
-#pragma unroll
-    for (int z = 0; z < 12; ++z) mm[z] = M[z];
-    float pw[3][3];
-#pragma unroll
-    for (int z = 0; z < 3; ++z) {
-      pw[z][0] = dot4(mm + 0, pobj[z][0], pobj[z][1], pobj[z][2]);
-      pw[z][1] = dot4(mm + 4, pobj[z][0], pobj[z][1], pobj[z][2]);
-      pw[z][2] = dot4(mm + 8, pobj[z][0], pobj[z][1], pobj[z][2]);
-    }
-    const float e1x = pw[1][0] - pw[0][0], e1y = pw[1][1] - pw[0][1], e1z = pw[1][2] - pw[0][2];
-    const float e2x = pw[2][0] - pw[0][0], e2y = pw[2][1] - pw[0][1], e2z = pw[2][2] - pw[0][2];
-    const float nx = e1y * e2z - e1z * e2y;
-    const float ny = e1z * e2x - e1x * e2z;
-    const float nz = e1x * e2y - e1y * e2x;
-    const float nn = (nx * nx + ny * ny) + nz * nz;
-    float cs = 0.0f;
-    if (nn > 0.0f) {
-      const float d = (nx * s.sun_dir[0] + ny * s.sun_dir[1]) + nz * s.sun_dir[2];
-      cs = fabsf(d / sqrtf(nn));
-    }
-#pragma unroll
-    for (int z = 0; z < 3; ++z) {
-      const float shade = s.ambient[z] + s.sun[z] * cs;
-      const int qq = (int)(shade * 256.0f + 0.5f);
-      rc.q[z] = min(max(qq, 0), 65535);
-    }
+  for (int z = 0; z < 3; ++z) {
+    const float* p = tp + 3 * z;
+    pobj[z][0] = p[0]; pobj[z][1] = p[1]; pobj[z][2] = p[2];
+    v[z].x = dot4(c + 0, p[0], p[1], p[2]);
+    v[z].y = dot4(c + 4, p[0], p[1], p[2]);
+    v[z].w = dot4(c + 8, p[0], p[1], p[2]);
   }
-  float e[3], ssum, invw;
-  hom_eval(rc.h.A, rc.h.B, rc.h.C, rc.h.invdet, px, py, e, ssum, invw);
+  Hom h;
+  hom_setup(v, h);
+#pragma unroll
+  for (int z = 0; z < 3; ++z) { e.A[z] = h.A[z]; e.B[z] = h.B[z]; e.C[z] = h.C[z]; }
+  e.invdet = h.invdet;
+  e.label = m.label;
+  const MatDesc mat = s.mats[m.material];
+  e.tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
+  e.base = (uint32_t)mat.base[0] | ((uint32_t)mat.base[1] << 8) | ((uint32_t)mat.base[2] << 16);
+  const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
+#pragma unroll
+  for (int z = 0; z < 6; ++z) e.uv[z] = e.tex >= 0 ? tu[z] : 0.0f;
+  float pw[3][3];
+#pragma unroll
+  for (int z = 0; z < 3; ++z) {
+    pw[z][0] = dot4(mm + 0, pobj[z][0], pobj[z][1], pobj[z][2]);
+    pw[z][1] = dot4(mm + 4, pobj[z][0], pobj[z][1], pobj[z][2]);
+    pw[z][2] = dot4(mm + 8, pobj[z][0], pobj[z][1], pobj[z][2]);
+  }
+  const float e1x = pw[1][0] - pw[0][0], e1y = pw[1][1] - pw[0][1], e1z = pw[1][2] - pw[0][2];
+  const float e2x = pw[2][0] - pw[0][0], e2y = pw[2][1] - pw[0][1], e2z = pw[2][2] - pw[0][2];
+  const float nx = e1y * e2z - e1z * e2y;
+  const float ny = e1z * e2x - e1x * e2z;
+  const float nz = e1x * e2y - e1y * e2x;
+  const float nn = (nx * nx + ny * ny) + nz * nz;
+  float cs = 0.0f;
+  if (nn > 0.0f) {
+    const float d = (nx * s.sun_dir[0] + ny * s.sun_dir[1]) + nz * s.sun_dir[2];
+    cs = fabsf(d / sqrtf(nn));
+  }
+  uint32_t q[3];
+#pragma unroll
+  for (int z = 0; z < 3; ++z) {
+    const float shade = s.ambient[z] + s.sun[z] * cs;
+    const int qq = (int)(shade * 256.0f + 0.5f);
+    q[z] = (uint32_t)min(max(qq, 0), 65535);
+  }
+  e.q01 = q[0] | (q[1] << 16);
+  e.q2 = q[2];
+}
+
+// Depth, instance id and RGB of pixel (px, py) covered by entry e.
+__device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry& e, int px, int py,
+                                            uint32_t& rgb_out, int32_t& id_out, float& depth_out) {
+  float ev[3], ssum, invw;
+  hom_eval(e.A, e.B, e.C, e.invdet, px, py, ev, ssum, invw);
   depth_out = 1.0f / invw;
-  id_out = rc.label;
+  id_out = e.label;
+  int base[3] = {(int)(e.base & 255u), (int)((e.base >> 8) & 255u), (int)((e.base >> 16) & 255u)};
   int alb[3];
-  if (rc.tex >= 0) {
+  if (e.tex >= 0) {
     float u, v;
     int c[4];
-    interp_uv(e, ssum, rc.uvv, u, v);
-    tex_sample(s, rc.tex, u, v, c);
+    interp_uv(ev, ssum, e.uv, u, v);
+    tex_sample(s, e.tex, u, v, c);
 #pragma unroll
-    for (int z = 0; z < 3; ++z) alb[z] = (c[z] * rc.base[z] + 127) / 255;
+    for (int z = 0; z < 3; ++z) alb[z] = (c[z] * base[z] + 127) / 255;
   } else {
 #pragma unroll
-    for (int z = 0; z < 3; ++z) alb[z] = rc.base[z];
+    for (int z = 0; z < 3; ++z) alb[z] = base[z];
   }
+  const int q[3] = {(int)(e.q01 & 0xFFFFu), (int)(e.q01 >> 16), (int)e.q2};
   uint32_t o = 0;
 #pragma unroll
-  for (int z = 0; z < 3; ++z) o |= (uint32_t)min((alb[z] * rc.q[z] + 128) >> 8, 255) << (8 * z);
+  for (int z = 0; z < 3; ++z) o |= (uint32_t)min((alb[z] * q[z] + 128) >> 8, 255) << (8 * z);
   rgb_out = o;
+}
+
+// Resolve-phase LDS (aliases the raster loop's): the tile's distinct winning
+// triangles in a 256-slot open-addressing table, each set up once by one
+// thread, then read by every pixel that shows it.
+constexpr uint32_t kShadeSlots = kBlock;
+constexpr int kShadeProbes = 16;
+struct ResolveLds {
+  uint32_t keys[kShadeSlots];       // uid or kNoAlpha (empty)
+  ShadeEntry tab[kShadeSlots];
+  uint32_t lstat[5][kMaxLdsLabels]; // per-label pixel count + box
+};
+
+// Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
+__device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
+  const uint32_t h = (uid * 2654435761u) >> 24;
+#pragma clang loop vectorize(disable) unroll(disable)
+  for (int p = 0; p < kShadeProbes; ++p) {
+    const uint32_t idx = (h + (uint32_t)p) & (kShadeSlots - 1u);
+    const uint32_t prev = atomicCAS(&keys[idx], kNoAlpha, uid);
+    if (prev == kNoAlpha || prev == uid) return (int)idx;
+  }
+  return -1;
 }
 
 template <int V>
@@ -900,8 +921,9 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
   __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
   __shared__ union Lds {
     RasterLds<V> r;                                  // raster loop
-    uint32_t lstat[5][kMaxLdsLabels];                // resolve: per-label pixel count + box
+    ResolveLds q;                                    // resolve
   } L;
+  static_assert(sizeof(ResolveLds) <= sizeof(RasterLds<V>), "resolve LDS must fit in the raster loop's");
   const int tid = threadIdx.x;
   const uint32_t tile = blockIdx.x, f = blockIdx.y;
   const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
@@ -920,33 +942,96 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
     if (tid == 0 && zb[0] == 0ull && b.inst) b.inst[0] = 0;
     return;
   }
-  const uint32_t nl = min(b.n_labels, (uint32_t)kMaxLdsLabels);
-  for (uint32_t l = tid; l < nl; l += kBlock) {
-    L.lstat[0][l] = 0; L.lstat[1][l] = 0xFFFFFFFFu; L.lstat[2][l] = 0xFFFFFFFFu; L.lstat[3][l] = 0; L.lstat[4][l] = 0;
+  // keypoint visibility against the finished z-buffer: W <= depth -> 2, else 1
+  // (depth = 1/invW of the winning key, the value the resolve writes)
+  if (b.n_kp && ((b.kp_tiles[(size_t)f * b.tile_words + (tile >> 5)] >> (tile & 31u)) & 1u)) {
+    for (uint32_t k = tid; k < b.n_kp; k += kBlock) {
+      const size_t o = (size_t)f * b.n_kp + k;
+      const uint32_t pp = b.kp_pix[o];
+      const int px = (int)(pp & 0xFFFFu) - ox, py = (int)(pp >> 16) - oy;
+      if (pp == 0xFFFFFFFFu || px < 0 || px >= kTile || py < 0 || py >= kTile) continue;
+      const unsigned long long key = zb[py * kTile + px];
+      const float d = key == kEmptyKey ? INFINITY : 1.0f / __uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32));
+      b.kp_vis[o] = (b.kp_w[o] <= d) ? 2 : 1;
+    }
   }
+  const uint32_t nl = min(b.n_labels, (uint32_t)kMaxLdsLabels);
+  uint32_t (*lstat)[kMaxLdsLabels] = L.q.lstat;
+  for (uint32_t l = tid; l < nl; l += kBlock) {
+    lstat[0][l] = 0; lstat[1][l] = 0xFFFFFFFFu; lstat[2][l] = 0xFFFFFFFFu; lstat[3][l] = 0; lstat[4][l] = 0;
+  }
+  L.q.keys[tid] = kNoAlpha;
   __syncthreads();
   // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads
   const int ly = tid >> 3, lx0 = (tid & 7) * 4;
   const int py = oy + ly;
+  const bool row_ok = py < (int)s.H;
+  unsigned long long key[4];
+  int slot[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int px = ox + lx0 + k;
+    key[k] = (row_ok && px < (int)s.W) ? zb[ly * kTile + lx0 + k] : kEmptyKey;
+    slot[k] = -1;
+    if (key[k] != kEmptyKey) {
+      if (k > 0 && key[k - 1] != kEmptyKey && (uint32_t)key[k - 1] == (uint32_t)key[k]) slot[k] = slot[k - 1];
+      else slot[k] = shade_slot(L.q.keys, (uint32_t)key[k]);
+    }
+  }
+  __syncthreads();
+  {  // one thread per occupied slot: set the triangle up once for the whole tile
+    const uint32_t u = L.q.keys[tid];
+    if (u != kNoAlpha) {
+      ShadeEntry e;
+      shade_setup(s, b, f, u, e);
+      L.q.tab[tid] = e;
+    }
+  }
+  __syncthreads();
   const size_t npx = (size_t)s.W * s.H;
-  if (py < (int)s.H) {
+  if (row_ok) {
     uint32_t rgb[4];
     int32_t ids[4];
     float dep[4];
-    ResolveCache rc;
+    uint32_t last_uid = 0xFFFFFFFFu;   // overflow path (probe run full): private setup
+    ShadeEntry own;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int px = ox + lx0 + k;
-      const unsigned long long key = px < (int)s.W ? zb[ly * kTile + lx0 + k] : kEmptyKey;
-      resolve_pixel(s, b, f, px, py, key, rc, rgb[k], ids[k], dep[k]);
-      const int32_t label = ids[k];
-      if (label >= 0 && (uint32_t)label < nl) {
-        atomicAdd(&L.lstat[0][label], 1u);
-        atomicMin(&L.lstat[1][label], (uint32_t)px);
-        atomicMin(&L.lstat[2][label], (uint32_t)py);
-        atomicMax(&L.lstat[3][label], (uint32_t)px);
-        atomicMax(&L.lstat[4][label], (uint32_t)py);
+      if (key[k] == kEmptyKey) {
+        rgb[k] = s.sky & 0xFFFFFFu;
+        ids[k] = -1;
+        dep[k] = INFINITY;
+      } else if (slot[k] >= 0) {
+        shade_pixel(s, L.q.tab[slot[k]], px, py, rgb[k], ids[k], dep[k]);
+      } else {
+        if ((uint32_t)key[k] != last_uid) {
+          last_uid = (uint32_t)key[k];
+          shade_setup(s, b, f, last_uid, own);
+        }
+        shade_pixel(s, own, px, py, rgb[k], ids[k], dep[k]);
       }
+    }
+    // label stats, one set of LDS atomics per run of equal labels
+    int32_t run = -1;
+    uint32_t cnt = 0, xmin = 0, xmax = 0;
+#pragma unroll
+    for (int k = 0; k <= 4; ++k) {
+      const int32_t lab = k < 4 ? ids[k] : -2;
+      if (lab != run) {
+        if (run >= 0 && (uint32_t)run < nl) {
+          atomicAdd(&lstat[0][run], cnt);
+          atomicMin(&lstat[1][run], xmin);
+          atomicMin(&lstat[2][run], (uint32_t)py);
+          atomicMax(&lstat[3][run], xmax);
+          atomicMax(&lstat[4][run], (uint32_t)py);
+        }
+        run = lab;
+        cnt = 0;
+        xmin = (uint32_t)(ox + lx0 + k);
+      }
+      ++cnt;
+      xmax = (uint32_t)(ox + lx0 + k);
     }
     const int px0 = ox + lx0;
     const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
@@ -975,13 +1060,13 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
     __syncthreads();
     uint32_t* st = b.stats + (size_t)f * b.n_labels * 5;
     for (uint32_t l = tid; l < nl; l += kBlock) {
-      const uint32_t cnt = L.lstat[0][l];
+      const uint32_t cnt = lstat[0][l];
       if (cnt) {
         atomicAdd(&st[l * 5 + 0], cnt);
-        atomicMin(&st[l * 5 + 1], L.lstat[1][l]);
-        atomicMin(&st[l * 5 + 2], L.lstat[2][l]);
-        atomicMax(&st[l * 5 + 3], L.lstat[3][l]);
-        atomicMax(&st[l * 5 + 4], L.lstat[4][l]);
+        atomicMin(&st[l * 5 + 1], lstat[1][l]);
+        atomicMin(&st[l * 5 + 2], lstat[2][l]);
+        atomicMax(&st[l * 5 + 3], lstat[3][l]);
+        atomicMax(&st[l * 5 + 4], lstat[4][l]);
       }
     }
   }
@@ -996,7 +1081,9 @@ __global__ void k_init_stats(uint32_t* st, uint32_t n) {
 }
 
 // ---------------------------------------------------------------------------
-// k_keypoints: projection + depth-tested visibility
+// k_keypoints: projection of the frame's keypoints (before k_raster).  The
+// depth test that turns "in view" (1) into "visible" (2) runs inside k_raster
+// against the finished z-buffer, so the depth image need not exist in HBM.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void project_one(const float* pv, const float* p, float Wf, float Hf, float nearc,
                                             float& u, float& v, int& vis, int& px, int& py) {
@@ -1025,14 +1112,16 @@ __global__ __launch_bounds__(256) void k_keypoints(SceneDev s, BatchDev b) {
   float u, v;
   int vis, px, py;
   project_one(pv, p, (float)s.W, (float)s.H, s.near_clip, u, v, vis, px, py);
+  const size_t o = (size_t)f * b.n_kp + k;
+  b.kp_uv[o * 2 + 0] = u;
+  b.kp_uv[o * 2 + 1] = v;
+  b.kp_vis[o] = vis;
+  b.kp_pix[o] = vis ? ((uint32_t)px | ((uint32_t)py << 16)) : 0xFFFFFFFFu;
+  b.kp_w[o] = dot4(pv + 8, p[0], p[1], p[2]);
   if (vis) {
-    const float Wc = dot4(pv + 8, p[0], p[1], p[2]);
-    const float d = b.depth[(size_t)f * s.W * s.H + (size_t)py * s.W + px];
-    vis = (Wc <= d) ? 2 : 1;
+    const uint32_t t = (uint32_t)(py / kTile) * s.tiles_x + (uint32_t)(px / kTile);
+    atomicOr(&b.kp_tiles[(size_t)f * b.tile_words + (t >> 5)], 1u << (t & 31u));
   }
-  b.kp_uv[((size_t)f * b.n_kp + k) * 2 + 0] = u;
-  b.kp_uv[((size_t)f * b.n_kp + k) * 2 + 1] = v;
-  b.kp_vis[(size_t)f * b.n_kp + k] = vis;
 }
 
 __global__ void k_project(const float* pts, uint32_t n, const float* pv, float Wf, float Hf, float nearc, float* uv,

@@ -145,7 +145,8 @@ int csg_get_batch_stats(csg_ctx* ctx, csg_batch_stats* st);
 /* Per-stage device time accumulated with HIP events recorded on the launch
  * stream for every batch since the last reset (no host sync inside the
  * timed loop).  Stages: setup = k_clip+k_setup, bin = k_count+k_scan+k_bin,
- * raster = k_raster (tile raster + resolve), keypoints = k_keypoints. */
+ * keypoints = k_keypoints (projection), raster = k_raster (tile raster,
+ * keypoint depth test, resolve). */
 typedef struct {
   uint32_t batches;          /* batches accumulated (capped at the ring size, 4096) */
   uint32_t frames;           /* frames in those batches */
