@@ -73,6 +73,7 @@ struct csg_ctx {
   std::vector<HostTexture> textures;
   bool tex_dirty = true;
   DevBuf<uint8_t> texels;
+  DevBuf<uint32_t> aquad;
   DevBuf<TexDesc> texd;
   float ambient[3] = {0.26f, 0.29f, 0.34f}, sun[3] = {0.78f, 0.78f, 0.78f}, sun_dir[3] = {0.7071f, 0.f, 0.7071f};
   uint32_t sky = 191u | (217u << 8) | (255u << 16);
@@ -170,6 +171,7 @@ void csg_destroy(csg_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->mats.release(); c->chunks.release();
   c->texels.release();
+  c->aquad.release();
   c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
   c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
   c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
@@ -357,11 +359,24 @@ static int sync_scene_state(csg_ctx* c) {
       total += (size_t)c->textures[k].w * c->textures[k].h;
     }
     HIP_TRY(c, c->texels.alloc(std::max<size_t>(total * 4, 4)));
+    HIP_TRY(c, c->aquad.alloc(std::max<size_t>(total, 1)));
     HIP_TRY(c, c->texd.alloc(std::max<size_t>(td.size(), 1)));
+    std::vector<uint32_t> quad;
     for (size_t k = 0; k < c->textures.size(); ++k)
-      if (c->textures[k].present)
-        HIP_TRY(c, hipMemcpy(c->texels.p + (size_t)td[k].offset * 4, c->textures[k].rgba.data(),
-                             c->textures[k].rgba.size(), hipMemcpyHostToDevice));
+      if (c->textures[k].present) {
+        const HostTexture& t = c->textures[k];
+        HIP_TRY(c, hipMemcpy(c->texels.p + (size_t)td[k].offset * 4, t.rgba.data(), t.rgba.size(),
+                             hipMemcpyHostToDevice));
+        // alpha quads: the four alphas of each texel's bilinear footprint (wrapped)
+        quad.resize((size_t)t.w * t.h);
+        for (uint32_t y = 0; y < t.h; ++y)
+          for (uint32_t x = 0; x < t.w; ++x) {
+            const uint32_t x1 = x + 1 == t.w ? 0 : x + 1, y1 = y + 1 == t.h ? 0 : y + 1;
+            auto a = [&](uint32_t xx, uint32_t yy) { return (uint32_t)t.rgba[((size_t)yy * t.w + xx) * 4 + 3]; };
+            quad[(size_t)y * t.w + x] = a(x, y) | (a(x1, y) << 8) | (a(x, y1) << 16) | (a(x1, y1) << 24);
+          }
+        HIP_TRY(c, hipMemcpy(c->aquad.p + td[k].offset, quad.data(), quad.size() * 4, hipMemcpyHostToDevice));
+      }
     if (!td.empty()) HIP_TRY(c, hipMemcpy(c->texd.p, td.data(), td.size() * sizeof(TexDesc), hipMemcpyHostToDevice));
     c->tex_dirty = false;
   }
@@ -416,7 +431,7 @@ static int ensure_work(csg_ctx* c, uint32_t F) {
 static SceneDev scene_dev(const csg_ctx* c) {
   SceneDev s{};
   s.tri_pos = c->tri_pos.p; s.tri_uv = c->tri_uv.p; s.inst = c->inst.p;
-  s.mats = c->mats.p; s.texd = c->texd.p; s.texels = c->texels.p; s.n_inst = c->n_inst;
+  s.mats = c->mats.p; s.texd = c->texd.p; s.texels = c->texels.p; s.aquad = c->aquad.p; s.n_inst = c->n_inst;
   for (int k = 0; k < 3; ++k) { s.ambient[k] = c->ambient[k]; s.sun[k] = c->sun[k]; s.sun_dir[k] = c->sun_dir[k]; }
   s.sky = c->sky;
   s.W = c->cfg.width; s.H = c->cfg.height;

@@ -61,7 +61,8 @@ struct SceneDev {
   const InstDesc* inst;        // [I]
   const MatDesc* mats;
   const TexDesc* texd;
-  const uint8_t* texels;
+  const uint8_t* texels;        // RGBA8, all textures back to back (TexDesc.offset in texels)
+  const uint32_t* aquad;        // alpha quads, same indexing (see tex_alpha)
   uint32_t n_inst;
   float ambient[3], sun[3], sun_dir[3];
   uint32_t sky;                // packed r | g<<8 | b<<16

@@ -91,6 +91,18 @@ __device__ __forceinline__ void interp_uv(const float* e, float ssum, const floa
 // Bilinear RGBA8, repeat wrap, 8-bit fixed weights (v flipped: row 0 = top).
 struct TexTap { uint32_t i00, i10, i01, i11; int wx, wy; };
 
+// fu mod n in [0, n) for an integer-valued |fu| < 2^23, without an integer
+// division: q may be off by one (approximate reciprocal), one correction fixes
+// it; q*n and fu - q*n are integers below 2^24, so every step is exact.
+__device__ __forceinline__ int wrap_index(float fu, int n) {
+  const float nf = (float)n;
+  const float q = floorf(fu * __builtin_amdgcn_rcpf(nf));
+  float r = fu - q * nf;
+  if (r < 0.0f) r += nf;
+  else if (r >= nf) r -= nf;
+  return (int)r;
+}
+
 __device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {
   float tu = u * (float)tw - 0.5f;
   float tv = (1.0f - v) * (float)th - 0.5f;
@@ -100,10 +112,7 @@ __device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {
   TexTap t;
   t.wx = (int)((tu - fu) * 256.0f);
   t.wy = (int)((tv - fv) * 256.0f);
-  int x0 = (int)fu % tw;
-  if (x0 < 0) x0 += tw;
-  int y0 = (int)fv % th;
-  if (y0 < 0) y0 += th;
+  const int x0 = wrap_index(fu, tw), y0 = wrap_index(fv, th);
   const int x1 = (x0 + 1 == tw) ? 0 : x0 + 1;
   const int y1 = (y0 + 1 == th) ? 0 : y0 + 1;
   t.i00 = (uint32_t)(y0 * tw + x0); t.i10 = (uint32_t)(y0 * tw + x1);
@@ -111,11 +120,15 @@ __device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {
   return t;
 }
 
+__device__ __forceinline__ int bilerp8(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, int wx, int wy) {
+  const int top = (int)c00 * (256 - wx) + (int)c10 * wx;
+  const int bot = (int)c01 * (256 - wx) + (int)c11 * wx;
+  return (top * (256 - wy) + bot * wy + 32768) >> 16;
+}
+
 __device__ __forceinline__ int tex_channel(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, int sh, int wx,
                                            int wy) {
-  const int top = (int)((c00 >> sh) & 255u) * (256 - wx) + (int)((c10 >> sh) & 255u) * wx;
-  const int bot = (int)((c01 >> sh) & 255u) * (256 - wx) + (int)((c11 >> sh) & 255u) * wx;
-  return (top * (256 - wy) + bot * wy + 32768) >> 16;
+  return bilerp8((c00 >> sh) & 255u, (c10 >> sh) & 255u, (c01 >> sh) & 255u, (c11 >> sh) & 255u, wx, wy);
 }
 
 __device__ __forceinline__ void tex_sample(const SceneDev& s, int tid, float u, float v, int out[4]) {
@@ -127,11 +140,19 @@ __device__ __forceinline__ void tex_sample(const SceneDev& s, int tid, float u, 
   for (int c = 0; c < 4; ++c) out[c] = tex_channel(c00, c10, c01, c11, 8 * c, k.wx, k.wy);
 }
 
-// Alpha channel only (the alpha test); `wh` = width | height << 16.
-__device__ __forceinline__ int tex_alpha(const uint8_t* texels, uint32_t offset, uint32_t wh, float u, float v) {
-  const TexTap k = tex_taps((int)(wh & 0xFFFFu), (int)(wh >> 16), u, v);
-  const uint32_t* base = reinterpret_cast<const uint32_t*>(texels) + offset;
-  return tex_channel(base[k.i00], base[k.i10], base[k.i01], base[k.i11], 24, k.wx, k.wy);
+// Alpha channel only (the alpha test), from the alpha-quad image: texel
+// (x, y) holds the alphas of (x,y), (x+1,y), (x,y+1), (x+1,y+1) (wrapped), so
+// the bilinear footprint is one 4-byte load.  `wh` = width | height << 16.
+__device__ __forceinline__ int tex_alpha(const uint32_t* aquad, uint32_t offset, uint32_t wh, float u, float v) {
+  const int tw = (int)(wh & 0xFFFFu), th = (int)(wh >> 16);
+  float tu = u * (float)tw - 0.5f;
+  float tv = (1.0f - v) * (float)th - 0.5f;
+  if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
+  if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
+  const float fu = floorf(tu), fv = floorf(tv);
+  const int wx = (int)((tu - fu) * 256.0f), wy = (int)((tv - fv) * 256.0f);
+  const uint32_t q = aquad[offset + (uint32_t)(wrap_index(fv, th) * tw + wrap_index(fu, tw))];
+  return bilerp8(q & 255u, (q >> 8) & 255u, (q >> 16) & 255u, q >> 24, wx, wy);
 }
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -629,7 +650,7 @@ __device__ __forceinline__ void row_span(const Rec& R, int ox, int oy, int ly, i
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
 struct RasterCtx {
-  const uint8_t* texels;
+  const uint32_t* aquad;
   unsigned long long* zb;
   int ox, oy;
   float inv_near, inv_far;
@@ -650,7 +671,7 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const Rec& R, int l
   if (!(c.dbg & 4u) && R.atex != kNoAlpha) {
     float u, v;
     interp_uv(e, ssum, R.uv, u, v);
-    if (!(tex_alpha(c.texels, R.atex, R.atex_wh, u, v) > (int)R.athr)) return;
+    if (!(tex_alpha(c.aquad, R.atex, R.atex_wh, u, v) > (int)R.athr)) return;
   }
   atomicMin(z, key);
 }
@@ -933,7 +954,7 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
   const uint32_t end = (b.dbg & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
   const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
-  RasterCtx c{s.texels, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg};
+  RasterCtx c{s.aquad, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg};
   __syncthreads();
   raster_block<V>(c, b, L.r, beg, end, bins, recs);
   __syncthreads();
