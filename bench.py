@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--frames-per-step", type=int, default=60)
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=48, help="frames rendered by the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=96, help="frames rendered by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
