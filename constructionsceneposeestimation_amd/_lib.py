@@ -11,7 +11,7 @@ from typing import Optional
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 1  # CSG_ABI_VERSION in include/csg_api.h
+ABI_VERSION = 2  # CSG_ABI_VERSION in include/csg_api.h
 
 EXPORTED = (
     "csg_create", "csg_destroy", "csg_last_error", "csg_abi_version", "csg_upload_scene",
@@ -60,7 +60,8 @@ class Frame(C.Structure):
 class Outputs(C.Structure):
     _fields_ = [("rgb", C.c_void_p), ("instance", C.c_void_p), ("depth", C.c_void_p),
                 ("keypoints_uv", C.c_void_p), ("keypoints_vis", C.c_void_p), ("inst_stats", C.c_void_p),
-                ("n_labels", C.c_uint32), ("on_device", C.c_int32)]
+                ("n_labels", C.c_uint32), ("on_device", C.c_int32), ("normals", C.c_void_p),
+                ("points", C.c_void_p)]
 
 
 class BatchStats(C.Structure):

@@ -14,6 +14,8 @@ build's additions.
   ``bboxDict_to_transform`` :562-564);
 * ``pointcloud`` -> ``{"data": (N,3) float32 world points, "pointRgb": (N,4)
   uint8, "info": {...}}`` (:1614, :1720-1724, :735);
+* ``normals`` -> H x W x 3 float16 unit world-space normals facing the camera
+  (0 on background; C5);
 * ``rgb`` -> H x W x 4 uint8;
 * ``bounding_box_2d_tight`` / ``keypoints_2d`` -> this build's per-instance
   pixel boxes and 2D keypoints (uv, visibility).
@@ -28,7 +30,9 @@ from . import sensors
 from .labels import bbox3d_records
 
 SUPPORTED = ("rgb", "distance_to_image_plane", "instance_segmentation", "bounding_box_3d",
-             "bounding_box_2d_tight", "pointcloud", "keypoints_2d")
+             "bounding_box_2d_tight", "pointcloud", "keypoints_2d", "normals")
+# renderer outputs an annotator needs beyond the camera's defaults
+_NEEDS = {"pointcloud": ("points",), "normals": ("normals",)}
 
 
 def unproject_depth(depth: np.ndarray, cam_to_world: np.ndarray, intr) -> np.ndarray:
@@ -54,6 +58,7 @@ class Annotator:
     def attach(self, render_product_path) -> None:
         paths = render_product_path if isinstance(render_product_path, (list, tuple)) else [render_product_path]
         self.camera = sensors.get_camera(paths[0])
+        self.camera.require(_NEEDS.get(self.name, ()))
 
     def detach(self) -> None:
         self.camera = None
@@ -92,11 +97,15 @@ class Annotator:
                 rec[n] = (scene.objects[j].class_id, s[1], s[2], s[3], s[4], s[0])
             return {"data": rec, "info": {"primPaths": [scene.objects[j].prim_path for j in vis]}}
         if self.name == "pointcloud":
-            pts, m = unproject_depth(out["depth"], meta["cam_to_world"], cam.intrinsics())
+            # world points unprojected on the GPU inside the resolve (fused)
+            m = np.isfinite(out["depth"])
+            pts = out["points"][m]
             rgb = out["rgb"][m]
             rgba = np.concatenate([rgb, np.full((rgb.shape[0], 1), 255, np.uint8)], 1)
             sem = out["instance"][m]
             return {"data": pts, "pointRgb": rgba, "info": {"pointInstance": sem}}
+        if self.name == "normals":
+            return out["normals"].copy()
         if self.name == "keypoints_2d":
             return {"data": out.get("keypoints_uv"), "visibility": out.get("keypoints_vis"),
                     "info": {"table": cam.stage.workload.kp_table}}

@@ -97,7 +97,8 @@ struct csg_ctx {
   // internal outputs (host-output mode / scratch)
   DevBuf<uint8_t> o_rgb;
   DevBuf<int32_t> o_inst;
-  DevBuf<float> o_depth, o_kp_uv, kp_w;
+  DevBuf<float> o_depth, o_kp_uv, kp_w, o_points, cam;
+  DevBuf<uint16_t> o_normals;
   DevBuf<int32_t> o_kp_vis;
   DevBuf<uint32_t> kp_pix, kp_tiles;
   DevBuf<uint32_t> o_stats;
@@ -177,6 +178,7 @@ void csg_destroy(csg_ctx* c) {
   c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
   c->kp_w.release(); c->kp_pix.release(); c->kp_tiles.release();
+  c->o_points.release(); c->o_normals.release(); c->cam.release();
   if (c->h_frames) (void)hipHostFree(c->h_frames);
   for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
@@ -414,6 +416,7 @@ static int ensure_work(csg_ctx* c, uint32_t F) {
   if (!c->h_frames) HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_frames), sizeof(FrameDev) * maxF));
   HIP_TRY(c, c->clip.alloc((size_t)maxF * c->n_inst * 12));
   HIP_TRY(c, c->pv.alloc((size_t)maxF * 12));
+  HIP_TRY(c, c->cam.alloc((size_t)maxF * kCamFloats));
   HIP_TRY(c, c->recs.alloc((size_t)maxF * c->rec_cap));
   HIP_TRY(c, c->rect.alloc((size_t)maxF * c->rec_cap));
   HIP_TRY(c, c->rec_count.alloc((size_t)maxF * kCounterStride));
@@ -475,6 +478,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   b.models = c->models.p;
   b.clip = c->clip.p;
   b.pv = c->pv.p;
+  b.cam = c->cam.p;
   b.recs = c->recs.p;
   b.rect = c->rect.p;
   b.rec_cap = c->rec_cap;
@@ -493,6 +497,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     b.rgb = out->rgb;
     b.inst = out->instance;
     b.depth = out->depth;
+    b.normals = out->normals;
+    b.points = out->points;
     b.stats = out->inst_stats;
     b.kp_uv = out->keypoints_uv;
     b.kp_vis = out->keypoints_vis;
@@ -500,6 +506,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (out->rgb) { HIP_TRY(c, c->o_rgb.alloc(F * npx * 3)); b.rgb = c->o_rgb.p; }
     if (out->instance) { HIP_TRY(c, c->o_inst.alloc(F * npx)); b.inst = c->o_inst.p; }
     if (out->depth) { HIP_TRY(c, c->o_depth.alloc(F * npx)); b.depth = c->o_depth.p; }
+    if (out->normals) { HIP_TRY(c, c->o_normals.alloc(F * npx * 3)); b.normals = c->o_normals.p; }
+    if (out->points) { HIP_TRY(c, c->o_points.alloc(F * npx * 3)); b.points = c->o_points.p; }
     if (out->inst_stats && out->n_labels) {
       HIP_TRY(c, c->o_stats.alloc((size_t)F * out->n_labels * 5));
       b.stats = c->o_stats.p;
@@ -548,6 +556,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (out->rgb) HIP_TRY(c, hipMemcpyAsync(out->rgb, b.rgb, F * npx * 3, hipMemcpyDeviceToHost, st));
     if (out->instance) HIP_TRY(c, hipMemcpyAsync(out->instance, b.inst, F * npx * 4, hipMemcpyDeviceToHost, st));
     if (out->depth) HIP_TRY(c, hipMemcpyAsync(out->depth, b.depth, F * npx * 4, hipMemcpyDeviceToHost, st));
+    if (out->normals) HIP_TRY(c, hipMemcpyAsync(out->normals, b.normals, F * npx * 6, hipMemcpyDeviceToHost, st));
+    if (out->points) HIP_TRY(c, hipMemcpyAsync(out->points, b.points, F * npx * 12, hipMemcpyDeviceToHost, st));
     if (b.stats)
       HIP_TRY(c, hipMemcpyAsync(out->inst_stats, b.stats, (size_t)F * out->n_labels * 5 * 4, hipMemcpyDeviceToHost, st));
     if (want_kp && out->keypoints_uv)

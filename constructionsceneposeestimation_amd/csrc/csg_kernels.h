@@ -15,6 +15,7 @@ constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
 constexpr int kMaxLdsLabels = 256;        // per-label pixel stats kept in LDS
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
 constexpr uint32_t kNoAlpha = 0xFFFFFFFFu;  // Rec::atex of a record without alpha test
+constexpr uint32_t kCamFloats = 16;         // per-frame unprojection constants (frame_camera)
 
 struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };   // host-side bookkeeping
 // Per instance, everything a kernel needs before touching its triangles (one load).
@@ -88,7 +89,10 @@ struct BatchDev {
   // outputs (device)
   uint8_t* rgb;                // [F][H][W][3] or null
   int32_t* inst;               // [F][H][W] or null
-  float* depth;                // [F][H][W] (internal scratch when the caller wants none)
+  float* depth;                // [F][H][W] or null
+  uint16_t* normals;           // [F][H][W][3] f16 bits or null
+  float* points;               // [F][H][W][3] world xyz (NaN: no hit) or null
+  float* cam;                  // [F][kCamFloats] camera-to-world rotation, position, fx fy cx cy
   uint32_t* stats;             // [F][n_labels][5] or null
   uint32_t n_labels;
   const float* kp;             // [n_sets][K][3]

@@ -208,6 +208,39 @@ __device__ __forceinline__ int find_item(const uint32_t* pre, uint32_t j) {
   return lo;
 }
 
+// Per-frame camera constants for unprojection (spec, same in csg_oracle.c):
+// camera-to-world rotation = transpose of the view rotation, camera position
+// c_i = -((V0i*t0 + V1i*t1) + V2i*t2), and fx, fy, cx, cy read back from the
+// pixel projection (rows u*w = fx*x - cx*z, v*w = -fy*y - cy*z, w = -z).
+__device__ __forceinline__ void frame_camera(const float* V, const float* P, float* cam) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) cam[i * 3 + j] = V[j * 4 + i];
+    cam[9 + i] = -((V[0 * 4 + i] * V[3] + V[1 * 4 + i] * V[7]) + V[2 * 4 + i] * V[11]);
+  }
+  cam[12] = P[0];
+  cam[13] = -P[5];
+  cam[14] = -P[2];
+  cam[15] = -P[6];
+}
+
+// World-space point on the ray through pixel (px, py)'s centre at distance-to-
+// image-plane d.
+__device__ __forceinline__ void unproject(const float* cam, int px, int py, float d, float out[3]) {
+  const float a = ((float)px + 0.5f) - cam[14], bq = ((float)py + 0.5f) - cam[15];
+  const float xc = (a * d) / cam[12], yc = -((bq * d) / cam[13]), zc = -d;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) out[i] = ((cam[i * 3 + 0] * xc + cam[i * 3 + 1] * yc) + cam[i * 3 + 2] * zc) + cam[9 + i];
+}
+
+// f16 bits of x rounded to nearest even; -0 is canonicalised to +0 first
+// (the spec's outputs carry no negative zeros).
+__device__ __forceinline__ uint32_t half_bits(float x) {
+  const _Float16 h = (_Float16)(x + 0.0f);   // v_cvt_f16_f32, round to nearest even
+  return (uint32_t)__builtin_bit_cast(uint16_t, h);
+}
+
 // ---------------------------------------------------------------------------
 // k_clip: per (frame, instance) clip rows of P*V*M; per frame P*V
 // ---------------------------------------------------------------------------
@@ -239,6 +272,7 @@ __global__ __launch_bounds__(256) void k_clip(SceneDev s, BatchDev b) {
       o[4 + k] = pv[4 + k];
       o[8 + k] = pv[12 + k];
     }
+    frame_camera(fr.view, fr.proj, b.cam + (size_t)f * kCamFloats);
   }
 }
 
@@ -821,6 +855,7 @@ struct ShadeEntry {
   int32_t tex;                      // -1: flat albedo
   uint32_t base;                    // albedo multiplier r | g << 8 | b << 16
   uint32_t q01, q2;                 // shade factors (x256): q0 | q1 << 16, q2
+  uint32_t n01, n2;                 // unit world normal facing the camera, f16: x | y << 16, z
 };
 
 // Triangle setup of the resolve, exactly as csg_oracle.c: clip coordinates,
@@ -872,9 +907,17 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   const float nz = e1x * e2y - e1y * e2x;
   const float nn = (nx * nx + ny * ny) + nz * nz;
   float cs = 0.0f;
+  e.n01 = 0;
+  e.n2 = 0;
   if (nn > 0.0f) {
+    const float len = sqrtf(nn);
     const float d = (nx * s.sun_dir[0] + ny * s.sun_dir[1]) + nz * s.sun_dir[2];
-    cs = fabsf(d / sqrtf(nn));
+    cs = fabsf(d / len);
+    // two-sided: the clip-space determinant is negative exactly when the face
+    // normal points toward the camera (pixel projection with fx*fy > 0)
+    const float sg = h.invdet < 0.0f ? 1.0f : -1.0f;
+    e.n01 = half_bits(sg * (nx / len)) | (half_bits(sg * (ny / len)) << 16);
+    e.n2 = half_bits(sg * (nz / len));
   }
   uint32_t q[3];
 #pragma unroll
@@ -1014,23 +1057,28 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
     uint32_t rgb[4];
     int32_t ids[4];
     float dep[4];
+    uint32_t nrm[4][2];
     uint32_t last_uid = 0xFFFFFFFFu;   // overflow path (probe run full): private setup
     ShadeEntry own;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int px = ox + lx0 + k;
+      nrm[k][0] = nrm[k][1] = 0;
       if (key[k] == kEmptyKey) {
         rgb[k] = s.sky & 0xFFFFFFu;
         ids[k] = -1;
         dep[k] = INFINITY;
       } else if (slot[k] >= 0) {
-        shade_pixel(s, L.q.tab[slot[k]], px, py, rgb[k], ids[k], dep[k]);
+        const ShadeEntry& e = L.q.tab[slot[k]];
+        shade_pixel(s, e, px, py, rgb[k], ids[k], dep[k]);
+        if (b.normals) { nrm[k][0] = e.n01; nrm[k][1] = e.n2; }
       } else {
         if ((uint32_t)key[k] != last_uid) {
           last_uid = (uint32_t)key[k];
           shade_setup(s, b, f, last_uid, own);
         }
         shade_pixel(s, own, px, py, rgb[k], ids[k], dep[k]);
+        if (b.normals) { nrm[k][0] = own.n01; nrm[k][1] = own.n2; }
       }
     }
     // label stats, one set of LDS atomics per run of equal labels
@@ -1056,7 +1104,28 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
     }
     const int px0 = ox + lx0;
     const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
-    if (px0 + 3 < (int)s.W) {
+    float pts[4][3];
+    if (b.points) {
+      const float* cam = b.cam + (size_t)f * kCamFloats;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (key[k] == kEmptyKey) pts[k][0] = pts[k][1] = pts[k][2] = __builtin_nanf("");
+        else unproject(cam, px0 + k, py, dep[k], pts[k]);
+      }
+    }
+    if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
+      if (b.normals) {   // 4 px x 3 halves = three 8-B words
+        uint2* d = reinterpret_cast<uint2*>(b.normals + o * 3);
+        d[0] = make_uint2(nrm[0][0], (nrm[0][1] & 0xFFFFu) | (nrm[1][0] << 16));
+        d[1] = make_uint2((nrm[1][0] >> 16) | (nrm[1][1] << 16), nrm[2][0]);
+        d[2] = make_uint2((nrm[2][1] & 0xFFFFu) | (nrm[3][0] << 16), (nrm[3][0] >> 16) | (nrm[3][1] << 16));
+      }
+      if (b.points) {    // 4 px x 3 floats = three 16-B words
+        float4* d = reinterpret_cast<float4*>(b.points + o * 3);
+        d[0] = make_float4(pts[0][0], pts[0][1], pts[0][2], pts[1][0]);
+        d[1] = make_float4(pts[1][1], pts[1][2], pts[2][0], pts[2][1]);
+        d[2] = make_float4(pts[2][2], pts[3][0], pts[3][1], pts[3][2]);
+      }
       if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(ids[0], ids[1], ids[2], ids[3]);
       if (b.depth) *reinterpret_cast<float4*>(b.depth + o) = make_float4(dep[0], dep[1], dep[2], dep[3]);
       if (b.rgb) {
@@ -1069,6 +1138,16 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
       for (int k = 0; k < 4 && px0 + k < (int)s.W; ++k) {
         if (b.inst) b.inst[o + k] = ids[k];
         if (b.depth) b.depth[o + k] = dep[k];
+        if (b.normals) {
+          b.normals[(o + k) * 3 + 0] = (uint16_t)(nrm[k][0] & 0xFFFFu);
+          b.normals[(o + k) * 3 + 1] = (uint16_t)(nrm[k][0] >> 16);
+          b.normals[(o + k) * 3 + 2] = (uint16_t)(nrm[k][1] & 0xFFFFu);
+        }
+        if (b.points) {
+          b.points[(o + k) * 3 + 0] = pts[k][0];
+          b.points[(o + k) * 3 + 1] = pts[k][1];
+          b.points[(o + k) * 3 + 2] = pts[k][2];
+        }
         if (b.rgb) {
           b.rgb[(o + k) * 3 + 0] = (uint8_t)(rgb[k] & 255u);
           b.rgb[(o + k) * 3 + 1] = (uint8_t)((rgb[k] >> 8) & 255u);

@@ -12,7 +12,8 @@ same files:
   labels/label_%06d.json           (:2071-2072, schema :2056-2064 + keypoints_2d)
   labels/instance_mask_%06d.npy    (:2066-2069; real ids here, -1 background)
   depth/depth_%06d.npy|.csv        (:1687-1688, optional)
-  pointcloud/pointcloud_%06d.txt   (:1716-1724, optional)
+  pointcloud/pointcloud_%06d.txt   (:1716-1724, optional; points from the GPU resolve)
+  normals/normals_%06d.npy         (C5 normals, f16, optional)
   logs/generation_summary.json     (:2090)
 
 Sharding: ``--rank/--world`` (or RANK/WORLD_SIZE) pick the epochs this
@@ -45,26 +46,28 @@ def _write_png(path: str, rgb: np.ndarray) -> None:
     Image.fromarray(rgb).save(path, compress_level=1)
 
 
-def _write_pointcloud(path: str, depth: np.ndarray, rgb: np.ndarray, cam_to_world: np.ndarray, intr) -> None:
-    from .annotators import unproject_depth
-    pts, m = unproject_depth(depth, cam_to_world, intr)
-    xyzrgb = np.hstack([pts.astype(np.float64), rgb[m].astype(np.float64)])
+def _write_pointcloud(path: str, points: np.ndarray, rgb: np.ndarray) -> None:
+    """``x y z r g b`` per hit pixel (generate_construction_data.py:769-770);
+    the world points come from the GPU resolve (NaN where nothing is hit)."""
+    m = np.isfinite(points[..., 0])
+    xyzrgb = np.hstack([points[m].astype(np.float64), rgb[m].astype(np.float64)])
     np.savetxt(path, xyzrgb, fmt="%.6f", delimiter=" ", header="x y z r g b", comments="")
 
 
 def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 30,
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 8,
-             resume: bool = True) -> dict:
+             resume: bool = True, normals: bool = False) -> dict:
     wl = Workload(workload, seed=seed, width=width, height=height)
-    for d in ("rgb", "labels", "depth", "pointcloud", "logs"):
+    for d in ("rgb", "labels", "depth", "pointcloud", "normals", "logs"):
         os.makedirs(os.path.join(out_dir, d), exist_ok=True)
     if resume:
         frames = [f for f in frames if not os.path.exists(os.path.join(out_dir, "labels", f"label_{f:06d}.json"))]
     log = QualityLog(os.path.join(out_dir, "logs"))
     r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
     intr = wl.intr
-    want = ["rgb", "instance", "keypoints", "stats"] + (["depth"] if (depth or pointcloud) else [])
+    want = (["rgb", "instance", "keypoints", "stats"] + (["depth"] if depth else [])
+            + (["points"] if pointcloud else []) + (["normals"] if normals else []))
     pose_cache = {}
     pool = ThreadPoolExecutor(max_workers=writers)
     pending = []
@@ -100,7 +103,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             if pointcloud:
                 pending.append(pool.submit(_write_pointcloud, os.path.join(out_dir, "pointcloud",
                                                                            f"pointcloud_{f:06d}.txt"),
-                                           out["depth"][k], out["rgb"][k], C, intr))
+                                           out["points"][k], out["rgb"][k]))
+            if normals:
+                pending.append(pool.submit(np.save, os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"),
+                                           out["normals"][k]))
         # bound the queue so host memory stays flat
         while len(pending) > 64 * max(writers, 1):
             pending.pop(0).result()
@@ -127,12 +133,13 @@ def main(argv=None):
     ap.add_argument("--depth", action="store_true")
     ap.add_argument("--depth-csv", action="store_true")
     ap.add_argument("--pointcloud", action="store_true")
+    ap.add_argument("--normals", action="store_true")
     ap.add_argument("--no-resume", action="store_true")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
-                       a.width, a.height, resume=not a.no_resume)
+                       a.width, a.height, resume=not a.no_resume, normals=a.normals)
     print(json.dumps(summary))
 
 

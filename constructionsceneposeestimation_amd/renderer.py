@@ -144,45 +144,41 @@ class Renderer:
         n = frames.shape[0]
         H, W = self.height, self.width
         out: Dict[str, np.ndarray] = {}
-        o = _lib.Outputs()
         if "rgb" in want:
             out["rgb"] = np.empty((n, H, W, 3), np.uint8)
-            o.rgb = out["rgb"].ctypes.data
         if "instance" in want:
             out["instance"] = np.empty((n, H, W), np.int32)
-            o.instance = out["instance"].ctypes.data
         if "depth" in want:
             out["depth"] = np.empty((n, H, W), np.float32)
-            o.depth = out["depth"].ctypes.data
         if "keypoints" in want and self.n_kp:
             out["keypoints_uv"] = np.empty((n, self.n_kp, 2), np.float32)
             out["keypoints_vis"] = np.empty((n, self.n_kp), np.int32)
-            o.keypoints_uv = out["keypoints_uv"].ctypes.data
-            o.keypoints_vis = out["keypoints_vis"].ctypes.data
         if "stats" in want:
             out["inst_stats"] = np.empty((n, self.n_labels, 5), np.uint32)
-            o.inst_stats = out["inst_stats"].ctypes.data
-        o.n_labels = self.n_labels
-        o.on_device = 0
+        if "normals" in want:
+            out["normals"] = np.empty((n, H, W, 3), np.float16)
+        if "points" in want:
+            out["points"] = np.empty((n, H, W, 3), np.float32)
         for s in range(0, n, self.max_frames):
             e = min(n, s + self.max_frames)
             oo = _lib.Outputs()
-            for name, arr, per in (("rgb", out.get("rgb"), None), ("instance", out.get("instance"), None),
-                                   ("depth", out.get("depth"), None), ("keypoints_uv", out.get("keypoints_uv"), None),
-                                   ("keypoints_vis", out.get("keypoints_vis"), None),
-                                   ("inst_stats", out.get("inst_stats"), None)):
+            for name, key in (("rgb", "rgb"), ("instance", "instance"), ("depth", "depth"),
+                              ("keypoints_uv", "keypoints_uv"), ("keypoints_vis", "keypoints_vis"),
+                              ("inst_stats", "inst_stats"), ("normals", "normals"), ("points", "points")):
+                arr = out.get(key)
                 if arr is not None:
                     setattr(oo, name, arr[s:e].ctypes.data)
-            oo.n_labels, oo.on_device = o.n_labels, 0
+            oo.n_labels, oo.on_device = self.n_labels, 0
             self._check(self.lib.csg_render_batch(self.ctx, frames[s:e].ctypes.data, e - s, C.byref(oo)),
                         "render_batch")
         return out
 
     def render_into(self, frames_ptr: int, n: int, frames_on_device: bool, rgb: int = 0, instance: int = 0,
-                    depth: int = 0, kp_uv: int = 0, kp_vis: int = 0, stats: int = 0, stream: int = 0) -> None:
+                    depth: int = 0, kp_uv: int = 0, kp_vis: int = 0, stats: int = 0, stream: int = 0,
+                    normals: int = 0, points: int = 0) -> None:
         """Enqueue a batch writing device buffers (raw pointers, e.g. torch ``data_ptr()``)."""
         o = _lib.Outputs(rgb or None, instance or None, depth or None, kp_uv or None, kp_vis or None,
-                         stats or None, self.n_labels, 1)
+                         stats or None, self.n_labels, 1, normals or None, points or None)
         self._check(self.lib.csg_render_batch_async(self.ctx, frames_ptr, n, int(frames_on_device), C.byref(o),
                                                     stream or None), "render_batch_async")
 

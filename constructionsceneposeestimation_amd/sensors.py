@@ -94,7 +94,16 @@ class Camera:
         self._frame_meta: Dict[str, object] = {}
         self._dirty = False
         self._frame_id = 0
+        self._extra: set = set()        # extra renderer outputs requested by attached annotators
         _CAMERAS[self.get_render_product_path()] = self
+
+    def require(self, outputs) -> None:
+        """Annotators attached to this camera ask for extra renderer outputs
+        (``points``, ``normals``); takes effect from the next frame."""
+        new = set(outputs) - self._extra
+        if new:
+            self._extra |= new
+            self._dirty = True
 
     # -- USD camera attributes (:1436-1443) -----------------------------------
     def set_clipping_range(self, near: float, far: float) -> None:
@@ -163,7 +172,7 @@ class Camera:
             self._uploaded_version = self.stage.version
         V, P, C = cm.frame_matrices(self._pos, self._quat, self.intrinsics())
         fr = make_frames(V[None], P[None], [0], [self._frame_id])
-        out = r.render(fr, want=("rgb", "instance", "depth", "keypoints", "stats"))
+        out = r.render(fr, want=("rgb", "instance", "depth", "keypoints", "stats") + tuple(sorted(self._extra)))
         self._frame = {k: v[0] for k, v in out.items()}
         self._frame_meta = {"view": V, "proj": P, "cam_to_world": C, "epoch": self.stage.epoch,
                             "frame_id": self._frame_id}

@@ -10,7 +10,7 @@ can be produced by any process independently.
 * C3  world2 + crane/dumper/4 rigged-human proxies, 1920x1080, RGB + instance
       segmentation + 2D keypoints (the bench workload)
 * C4  C3 with per-epoch randomisation, frames seed-sharded across GPUs
-* C5  C3 at 3840x2160 with depth output
+* C5  C3 at 3840x2160 with depth, normals (f16) and world points
 """
 from __future__ import annotations
 
@@ -31,7 +31,8 @@ WORKLOADS = {
     "C2": dict(scene="world2", width=1920, height=1080, outputs=("rgb", "instance")),
     "C3": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints")),
     "C4": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints")),
-    "C5": dict(scene="world2_people", width=3840, height=2160, outputs=("rgb", "instance", "depth", "keypoints")),
+    "C5": dict(scene="world2_people", width=3840, height=2160,
+               outputs=("rgb", "instance", "depth", "normals", "points", "keypoints")),
 }
 
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 1
+#define CSG_ABI_VERSION 2
 
 typedef enum {
   CSG_OK = 0,
@@ -109,6 +109,10 @@ typedef struct {
   uint32_t* inst_stats;      /* [n][n_labels][5] = pixels, minx, miny, maxx, maxy */
   uint32_t n_labels;
   int32_t on_device;         /* 1: device pointers (stay in HBM), 0: host pointers */
+  uint16_t* normals;         /* [n][H][W][3] f16 bits: unit world-space face normal facing
+                                the camera; 0 where nothing is hit (C5 normals) */
+  float* points;             /* [n][H][W][3] world-space point of each pixel from its depth
+                                (depth_to_pointcloud GDP:616-711, fused); NaN where no hit */
 } csg_outputs;
 
 typedef struct {

@@ -223,9 +223,63 @@ static void build_clip(const oracle_scene* s, const float* view, const float* pr
   ic->mat = &s->materials[ic->m->material];
 }
 
+/* float -> IEEE half, round to nearest even (bit pattern). */
+static uint16_t f32_to_f16(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t e8 = (x >> 23) & 0xffu;
+  uint32_t mant = x & 0x7fffffu;
+  if (e8 == 0xffu) return (uint16_t)(sign | 0x7c00u | (mant ? 0x200u : 0u));
+  const int32_t e = (int32_t)e8 - 127 + 15;
+  if (e >= 31) return (uint16_t)(sign | 0x7c00u);
+  if (e <= 0) {                      /* half subnormal or zero */
+    if (e < -10) return (uint16_t)sign;
+    mant |= 0x800000u;
+    const uint32_t shift = (uint32_t)(14 - e);
+    uint32_t hm = mant >> shift;
+    const uint32_t rem = mant & ((1u << shift) - 1u), halfway = 1u << (shift - 1u);
+    if (rem > halfway || (rem == halfway && (hm & 1u))) hm++;
+    return (uint16_t)(sign | hm);
+  }
+  uint32_t h = sign | ((uint32_t)e << 10) | (mant >> 13);
+  const uint32_t rem = mant & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+  return (uint16_t)h;
+}
+
+/* Per-frame unprojection constants: camera-to-world rotation (transpose of
+ * the view rotation), camera position -R^T t, fx, fy, cx, cy read back from
+ * the pixel projection. */
+static void frame_camera(const float* V, const float* P, float* cam) {
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) cam[i * 3 + j] = V[j * 4 + i];
+    cam[9 + i] = -((V[0 * 4 + i] * V[3] + V[1 * 4 + i] * V[7]) + V[2 * 4 + i] * V[11]);
+  }
+  cam[12] = P[0];
+  cam[13] = -P[5];
+  cam[14] = -P[2];
+  cam[15] = -P[6];
+}
+
+/* World point on the ray through the pixel centre at distance-to-image-plane d
+ * (the depth_to_pointcloud step, generate_construction_data.py:616-711, in
+ * the USD camera convention). */
+static void unproject(const float* cam, int px, int py, float d, float* out) {
+  const float a = ((float)px + 0.5f) - cam[14], b = ((float)py + 0.5f) - cam[15];
+  const float xc = (a * d) / cam[12], yc = -((b * d) / cam[13]), zc = -d;
+  for (int i = 0; i < 3; ++i) out[i] = ((cam[i * 3 + 0] * xc + cam[i * 3 + 1] * yc) + cam[i * 3 + 2] * zc) + cam[9 + i];
+}
+
 int oracle_render_frame(const oracle_scene* s, const float* view, const float* proj,
                         uint8_t* rgb, int32_t* inst, float* depth,
                         uint32_t* inst_stats, uint32_t n_labels, oracle_stats* st_out) {
+  return oracle_render_frame_ex(s, view, proj, rgb, inst, depth, NULL, NULL, inst_stats, n_labels, st_out);
+}
+
+int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float* proj,
+                           uint8_t* rgb, int32_t* inst, float* depth, uint16_t* normals, float* points,
+                           uint32_t* inst_stats, uint32_t n_labels, oracle_stats* st_out) {
   const int W = (int)s->width, H = (int)s->height;
   uint64_t* zbuf = (uint64_t*)malloc((size_t)W * H * sizeof(uint64_t));
   if (!zbuf) return -1;
@@ -295,6 +349,8 @@ int oracle_render_frame(const oracle_scene* s, const float* view, const float* p
   }
 
   /* resolve */
+  float cam[16];
+  frame_camera(view, proj, cam);
   if (inst_stats && n_labels) {
     for (uint32_t l = 0; l < n_labels; ++l) {
       inst_stats[l * 5 + 0] = 0;
@@ -312,6 +368,8 @@ int oracle_render_frame(const oracle_scene* s, const float* view, const float* p
         if (rgb) { rgb[p * 3 + 0] = s->sky[0]; rgb[p * 3 + 1] = s->sky[1]; rgb[p * 3 + 2] = s->sky[2]; }
         if (inst) inst[p] = -1;
         if (depth) depth[p] = INFINITY;
+        if (normals) normals[p * 3 + 0] = normals[p * 3 + 1] = normals[p * 3 + 2] = 0;
+        if (points) points[p * 3 + 0] = points[p * 3 + 1] = points[p * 3 + 2] = NAN;
         continue;
       }
       const uint32_t uid = (uint32_t)key;
@@ -328,6 +386,7 @@ int oracle_render_frame(const oracle_scene* s, const float* view, const float* p
       hom_eval(&h, px, py, e, &ssum, &invw);
       const int32_t label = s->inst_label[i];
       if (depth) depth[p] = 1.0f / invw;
+      if (points) unproject(cam, px, py, 1.0f / invw, points + p * 3);
       if (inst) inst[p] = label;
       if (inst_stats && label >= 0 && (uint32_t)label < n_labels) {
         uint32_t* q = inst_stats + (size_t)label * 5;
@@ -337,7 +396,7 @@ int oracle_render_frame(const oracle_scene* s, const float* view, const float* p
         if ((uint32_t)px > q[3]) q[3] = (uint32_t)px;
         if ((uint32_t)py > q[4]) q[4] = (uint32_t)py;
       }
-      if (!rgb) continue;
+      if (!rgb && !normals) continue;
       int alb[3];
       const oracle_material* mat = ic.mat;
       if (mat->texture >= 0 && ic.m->has_uv) {
@@ -366,10 +425,20 @@ int oracle_render_frame(const oracle_scene* s, const float* view, const float* p
       const float nz = e1x * e2y - e1y * e2x;
       const float nn = (nx * nx + ny * ny) + nz * nz;
       float c = 0.0f;
+      uint16_t nh[3] = {0, 0, 0};
       if (nn > 0.0f) {
+        const float len = sqrtf(nn);
         const float d = (nx * s->sun_dir[0] + ny * s->sun_dir[1]) + nz * s->sun_dir[2];
-        c = fabsf(d / sqrtf(nn));
+        c = fabsf(d / len);
+        /* two-sided normal: det(clip) < 0 exactly when the face points at the camera */
+        const float sg = h.invdet < 0.0f ? 1.0f : -1.0f;
+        /* + 0.0f: no negative zeros in the output */
+        nh[0] = f32_to_f16(sg * (nx / len) + 0.0f);
+        nh[1] = f32_to_f16(sg * (ny / len) + 0.0f);
+        nh[2] = f32_to_f16(sg * (nz / len) + 0.0f);
       }
+      if (normals) { normals[p * 3 + 0] = nh[0]; normals[p * 3 + 1] = nh[1]; normals[p * 3 + 2] = nh[2]; }
+      if (!rgb) continue;
       for (int k = 0; k < 3; ++k) {
         const float shade = s->ambient[k] + s->sun[k] * c;
         int q = (int)(shade * 256.0f + 0.5f);

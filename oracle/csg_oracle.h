@@ -74,6 +74,13 @@ int oracle_render_frame(const oracle_scene* s, const float* view, const float* p
                         uint8_t* rgb, int32_t* inst, float* depth,
                         uint32_t* inst_stats, uint32_t n_labels, oracle_stats* st);
 
+/* Same plus the C5 outputs: normals [H][W][3] f16 bits (unit world-space face
+ * normal facing the camera, 0 for background) and points [H][W][3] (world
+ * point of each pixel from its depth, NaN for background). */
+int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float* proj,
+                           uint8_t* rgb, int32_t* inst, float* depth, uint16_t* normals, float* points,
+                           uint32_t* inst_stats, uint32_t n_labels, oracle_stats* st);
+
 /* Project world keypoints; visibility against a rendered depth buffer.
  * uv: [n][2], vis: [n] (0 out/behind, 1 occluded, 2 visible). */
 int oracle_keypoints(const oracle_scene* s, const float* view, const float* proj,

@@ -55,6 +55,8 @@ def lib():
         _lib = C.CDLL(build())
         vp, u32 = C.c_void_p, C.c_uint32
         _lib.oracle_render_frame.argtypes = [C.POINTER(_Scene), vp, vp, vp, vp, vp, vp, u32, C.POINTER(_Stats)]
+        _lib.oracle_render_frame_ex.argtypes = [C.POINTER(_Scene), vp, vp, vp, vp, vp, vp, vp, vp, u32,
+                                                C.POINTER(_Stats)]
         _lib.oracle_keypoints.argtypes = [C.POINTER(_Scene), vp, vp, vp, u32, vp, vp, vp]
         _lib.oracle_render_frames.argtypes = [C.POINTER(_Scene), vp, vp, u32, vp, vp, vp, vp, C.c_int]
         _lib.oracle_mat4_mul.argtypes = [vp, vp, vp]
@@ -113,21 +115,27 @@ class Oracle:
         self._keep.append(a)
         self.s.inst_model = a.ctypes.data
 
-    def render(self, view: np.ndarray, proj: np.ndarray, want_stats: bool = False):
+    def render(self, view: np.ndarray, proj: np.ndarray, want_stats: bool = False, extra: bool = False):
+        """One frame; ``extra`` adds the C5 outputs ``normals`` (H,W,3 float16)
+        and ``points`` (H,W,3 float32 world xyz, NaN where nothing is hit)."""
         H, W = self.height, self.width
         rgb = np.empty((H, W, 3), np.uint8)
         inst = np.empty((H, W), np.int32)
         depth = np.empty((H, W), np.float32)
+        normals = np.empty((H, W, 3), np.float16) if extra else None
+        points = np.empty((H, W, 3), np.float32) if extra else None
         nl = max(int(self.p.n_labels), 1)
         stats = np.empty((nl, 5), np.uint32)
         st = _Stats()
         v = np.ascontiguousarray(view, np.float32).reshape(16)
         pr = np.ascontiguousarray(proj, np.float32).reshape(16)
-        rc = lib().oracle_render_frame(C.byref(self.s), _ptr(v), _ptr(pr), _ptr(rgb), _ptr(inst), _ptr(depth),
-                                       _ptr(stats), nl, C.byref(st))
+        rc = lib().oracle_render_frame_ex(C.byref(self.s), _ptr(v), _ptr(pr), _ptr(rgb), _ptr(inst), _ptr(depth),
+                                          _ptr(normals), _ptr(points), _ptr(stats), nl, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_render_frame failed: {rc}")
         out = {"rgb": rgb, "instance": inst, "depth": depth, "inst_stats": stats}
+        if extra:
+            out["normals"], out["points"] = normals, points
         if want_stats:
             out["stats"] = {n: int(getattr(st, n)) for n, _ in _Stats._fields_}
         return out

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     for f in declared_functions():
         assert hasattr(lib, f), f
     assert set(declared_functions()) == set(_lib.EXPORTED)
-    assert lib.csg_abi_version() == 1
+    assert lib.csg_abi_version() == _lib.ABI_VERSION
 
 
 def test_invalid_config_rejected_without_gpu():

@@ -123,3 +123,50 @@ def test_oracle_deterministic_and_parallel_consistent(world2):
         one = o.render(views[k], projs[k])
         assert np.array_equal(one["rgb"], rgb[k]) and np.array_equal(one["instance"], inst[k])
         assert np.array_equal(one["depth"].view(np.uint32), depth[k].view(np.uint32))
+
+
+def test_normals_face_camera_and_points_unproject_depth(world2):
+    """C5 outputs of the spec: unit world-space face normals turned toward the
+    camera (two-sided), zero on background; world points from depth match the
+    float64 unprojection (annotators.unproject_depth, the pinhole of
+    generate_construction_data.py:646-649) to float32 rounding, NaN on
+    background."""
+    from constructionsceneposeestimation_amd.annotators import unproject_depth
+    W, H = 160, 96
+    o = Oracle(pack_scene(world2), W, H)
+    intr = cm.Intrinsics(W, H)
+    for cam, aim in [([-3.0, -3.0, 1.6], [0.0, 0.0, 1.6]), ([5.0, -5.0, 2.0], [0.0, 0.0, 0.5])]:
+        V, P, Cw = cm.frame_matrices(cam, cm.look_at_world_quat(cam, aim), intr)
+        out = o.render(V, P, extra=True)
+        hit = np.isfinite(out["depth"])
+        n = out["normals"].astype(np.float32)
+        pts = out["points"]
+        assert hit.any() and (~hit).any()
+        assert np.all(n[~hit] == 0) and np.all(np.isnan(pts[~hit]))
+        assert np.all(np.isfinite(pts[hit]))
+        ln = np.linalg.norm(n[hit], axis=-1)
+        nz = ln > 0
+        assert np.allclose(ln[nz], 1.0, atol=2e-3)
+        ref, m = unproject_depth(out["depth"], Cw, intr)
+        assert np.array_equal(m, hit)
+        err = np.linalg.norm(pts[hit].astype(np.float64) - ref, axis=-1)
+        assert err.max() < 1e-4 * max(1.0, float(out["depth"][hit].max()))
+        to_cam = np.asarray(cam, np.float64) - pts[hit].astype(np.float64)
+        facing = np.einsum("ij,ij->i", n[hit].astype(np.float64), to_cam)
+        assert (facing[nz] > -1e-3).all()
+
+
+def test_ground_normal_points_up_from_above():
+    W, H = 32, 24
+    o = Oracle(pack_scene(quad_scene()), W, H)
+    C = np.eye(4)
+    C[:3, 3] = [0.0, 0.0, 3.0]
+    out = o.render(cm.view_matrix(C), cm.Intrinsics(W, H).pixel_projection(), extra=True)
+    n = out["normals"].astype(np.float32)
+    assert np.array_equal(n.reshape(-1, 3), np.tile([0.0, 0.0, 1.0], (W * H, 1)).astype(np.float32))
+    # looking up at the same quad from below flips it
+    C[:3, :3] = np.diag([1.0, -1.0, -1.0])
+    C[:3, 3] = [0.0, 0.0, -3.0]
+    out = o.render(cm.view_matrix(C), cm.Intrinsics(W, H).pixel_projection(), extra=True)
+    n = out["normals"].astype(np.float32)
+    assert np.array_equal(n.reshape(-1, 3), np.tile([0.0, 0.0, -1.0], (W * H, 1)).astype(np.float32))
