@@ -65,8 +65,8 @@ struct csg_ctx {
   uint64_t n_tris_total = 0;
   DevBuf<float> tri_pos, tri_uv;       // de-indexed triangle soup (see SceneDev)
   DevBuf<InstDesc> inst;
-  DevBuf<MatDesc> mats;
   std::vector<MatDesc> h_mats;
+  std::vector<MatDesc> h_set_mats;      // [sets][n_materials] as uploaded
   std::vector<MeshDesc> h_meshes;
   DevBuf<Chunk> chunks;
   uint32_t n_chunks = 0;
@@ -75,8 +75,16 @@ struct csg_ctx {
   DevBuf<uint8_t> texels;
   DevBuf<uint32_t> aquad;
   DevBuf<TexDesc> texd;
-  float ambient[3] = {0.26f, 0.29f, 0.34f}, sun[3] = {0.78f, 0.78f, 0.78f}, sun_dir[3] = {0.7071f, 0.f, 0.7071f};
-  uint32_t sky = 191u | (217u << 8) | (255u << 16);
+  LightDev light{{0.26f, 0.29f, 0.34f}, {0.78f, 0.78f, 0.78f}, {0.7071f, 0.f, 0.7071f},
+                 191u | (217u << 8) | (255u << 16)};   // default (csg_set_light)
+  // domain randomisation per transform set (csg_set_dr_light / csg_set_dr_textures)
+  std::vector<LightDev> dr_light;
+  std::vector<uint8_t> dr_light_valid;
+  std::vector<int32_t> dr_tex;          // [sets][n_materials]; kKeepTexture = the material's own
+  bool dr_dirty = true;
+  DevBuf<LightDev> lights;
+  DevBuf<MatDesc> set_mats;
+  uint32_t n_table_sets = 0;
   std::vector<float> h_models;          // [sets][I][16]
   std::vector<uint8_t> set_valid;
   DevBuf<float> models;
@@ -170,7 +178,8 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
 void csg_destroy(csg_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->mats.release(); c->chunks.release();
+  c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->set_mats.release(); c->lights.release();
+  c->chunks.release();
   c->texels.release();
   c->aquad.release();
   c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
@@ -269,12 +278,10 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   if (ch.empty()) return c->fail(CSG_ERR_INVALID, "upload_scene: no triangles");
   HIP_TRY(c, c->tri_pos.alloc(std::max<size_t>(tri_pos.size(), 9)));
   HIP_TRY(c, c->tri_uv.alloc(std::max<size_t>(tri_uv.size(), 6)));
-  HIP_TRY(c, c->mats.alloc(n_materials));
   HIP_TRY(c, c->inst.alloc(n_inst));
   HIP_TRY(c, c->chunks.alloc(ch.size()));
   HIP_TRY(c, hipMemcpy(c->tri_pos.p, tri_pos.data(), tri_pos.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->tri_uv.p, tri_uv.data(), tri_uv.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->mats.p, mats.data(), mats.size() * sizeof(MatDesc), hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->inst.p, idesc.data(), idesc.size() * sizeof(InstDesc), hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->chunks.p, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice));
   c->n_inst = n_inst;
@@ -287,6 +294,8 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   c->h_models = models;
   c->set_valid.assign(1, 1);
   c->models_dirty = true;
+  c->dr_tex.clear();
+  c->dr_dirty = true;
   c->h_kp.clear();
   c->kp_valid.clear();
   c->n_kp = 0;
@@ -310,14 +319,49 @@ int csg_upload_texture(csg_ctx* c, uint32_t tex_id, const uint8_t* rgba8, uint32
   return CSG_OK;
 }
 
+static LightDev to_light(const csg_light* L) {
+  LightDev d;
+  for (int k = 0; k < 3; ++k) {
+    d.ambient[k] = L->ambient[k];
+    d.sun[k] = L->sun[k];
+    d.sun_dir[k] = L->sun_dir[k];
+  }
+  d.sky = (uint32_t)L->sky[0] | ((uint32_t)L->sky[1] << 8) | ((uint32_t)L->sky[2] << 16);
+  return d;
+}
+
 int csg_set_light(csg_ctx* c, const csg_light* L) {
   if (!c || !L) return CSG_ERR_INVALID;
-  for (int k = 0; k < 3; ++k) {
-    c->ambient[k] = L->ambient[k];
-    c->sun[k] = L->sun[k];
-    c->sun_dir[k] = L->sun_dir[k];
+  c->light = to_light(L);
+  c->dr_dirty = true;
+  return CSG_OK;
+}
+
+int csg_set_dr_light(csg_ctx* c, uint32_t set_id, const csg_light* L) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!L || set_id >= 4096) return c->fail(CSG_ERR_INVALID, "set_dr_light: need a light and set < 4096");
+  if (c->dr_light_valid.size() <= set_id) {
+    c->dr_light_valid.resize(set_id + 1, 0);
+    c->dr_light.resize(set_id + 1);
   }
-  c->sky = (uint32_t)L->sky[0] | ((uint32_t)L->sky[1] << 8) | ((uint32_t)L->sky[2] << 16);
+  c->dr_light[set_id] = to_light(L);
+  c->dr_light_valid[set_id] = 1;
+  c->dr_dirty = true;
+  return CSG_OK;
+}
+
+int csg_set_dr_textures(csg_ctx* c, uint32_t set_id, const int32_t* tex, uint32_t n) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "set_dr_textures: no scene");
+  if (!tex || n != c->n_materials || set_id >= 4096)
+    return c->fail(CSG_ERR_INVALID, "set_dr_textures: need %u entries, set < 4096", c->n_materials);
+  for (uint32_t m = 0; m < n; ++m)
+    if (tex[m] < CSG_KEEP_TEXTURE || tex[m] >= 4096)
+      return c->fail(CSG_ERR_INVALID, "set_dr_textures: material %u: bad texture id %d", m, tex[m]);
+  const size_t need = ((size_t)set_id + 1) * c->n_materials;
+  if (c->dr_tex.size() < need) c->dr_tex.resize(need, CSG_KEEP_TEXTURE);
+  memcpy(&c->dr_tex[(size_t)set_id * c->n_materials], tex, n * sizeof(int32_t));
+  c->dr_dirty = true;
   return CSG_OK;
 }
 
@@ -382,10 +426,33 @@ static int sync_scene_state(csg_ctx* c) {
     if (!td.empty()) HIP_TRY(c, hipMemcpy(c->texd.p, td.data(), td.size() * sizeof(TexDesc), hipMemcpyHostToDevice));
     c->tex_dirty = false;
   }
-  for (uint32_t m = 0; m < c->n_materials; ++m) {
-    const int t = c->h_mats[m].texture;
+  // per-set material and light tables (every set that has transforms)
+  const uint32_t n_sets = (uint32_t)c->set_valid.size();
+  if (c->dr_dirty || c->n_table_sets != n_sets) {
+    std::vector<MatDesc> sm((size_t)n_sets * c->n_materials);
+    std::vector<LightDev> sl(n_sets);
+    for (uint32_t set = 0; set < n_sets; ++set) {
+      sl[set] = (set < c->dr_light_valid.size() && c->dr_light_valid[set]) ? c->dr_light[set] : c->light;
+      for (uint32_t m = 0; m < c->n_materials; ++m) {
+        MatDesc d = c->h_mats[m];
+        const size_t k = (size_t)set * c->n_materials + m;
+        if (k < c->dr_tex.size() && c->dr_tex[k] != CSG_KEEP_TEXTURE) d.texture = c->dr_tex[k];
+        sm[(size_t)set * c->n_materials + m] = d;
+      }
+    }
+    HIP_TRY(c, c->set_mats.alloc(std::max<size_t>(sm.size(), 1)));
+    HIP_TRY(c, c->lights.alloc(std::max<size_t>(sl.size(), 1)));
+    c->h_set_mats = sm;
+    if (!sm.empty()) HIP_TRY(c, hipMemcpy(c->set_mats.p, sm.data(), sm.size() * sizeof(MatDesc), hipMemcpyHostToDevice));
+    if (!sl.empty()) HIP_TRY(c, hipMemcpy(c->lights.p, sl.data(), sl.size() * sizeof(LightDev), hipMemcpyHostToDevice));
+    c->n_table_sets = n_sets;
+    c->dr_dirty = false;
+  }
+  for (size_t k = 0; k < c->h_set_mats.size(); ++k) {
+    const int t = c->h_set_mats[k].texture;
     if (t >= 0 && ((size_t)t >= c->textures.size() || !c->textures[t].present))
-      return c->fail(CSG_ERR_INVALID, "material %u references texture %d that was not uploaded", m, t);
+      return c->fail(CSG_ERR_INVALID, "material %u (set %u) references texture %d that was not uploaded",
+                     (unsigned)(k % c->n_materials), (unsigned)(k / c->n_materials), t);
   }
   if (c->models_dirty) {
     HIP_TRY(c, c->models.alloc(c->h_models.size()));
@@ -434,9 +501,7 @@ static int ensure_work(csg_ctx* c, uint32_t F) {
 static SceneDev scene_dev(const csg_ctx* c) {
   SceneDev s{};
   s.tri_pos = c->tri_pos.p; s.tri_uv = c->tri_uv.p; s.inst = c->inst.p;
-  s.mats = c->mats.p; s.texd = c->texd.p; s.texels = c->texels.p; s.aquad = c->aquad.p; s.n_inst = c->n_inst;
-  for (int k = 0; k < 3; ++k) { s.ambient[k] = c->ambient[k]; s.sun[k] = c->sun[k]; s.sun_dir[k] = c->sun_dir[k]; }
-  s.sky = c->sky;
+  s.texd = c->texd.p; s.texels = c->texels.p; s.aquad = c->aquad.p; s.n_inst = c->n_inst;
   s.W = c->cfg.width; s.H = c->cfg.height;
   s.tiles_x = c->tiles_x; s.tiles_y = c->tiles_y; s.n_tiles = c->n_tiles;
   s.near_clip = c->cfg.near_clip; s.far_clip = c->cfg.far_clip;
@@ -476,6 +541,9 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   }
   b.frames = dframes;
   b.models = c->models.p;
+  b.mats = c->set_mats.p;
+  b.lights = c->lights.p;
+  b.n_mat = c->n_materials;
   b.clip = c->clip.p;
   b.pv = c->pv.p;
   b.cam = c->cam.p;

@@ -22,6 +22,10 @@ struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };   /
 struct InstDesc { uint32_t tbase, material, has_uv; int32_t label; };
 struct MatDesc { uint8_t base[4]; int32_t texture; uint32_t alpha_test, alpha_threshold; };
 struct TexDesc { uint32_t offset, width, height, pad; };
+// Lighting of one transform set (randomisation epoch): dome (ambient) and
+// distant-light contributions per channel, unit direction toward the sun,
+// background colour r | g << 8 | b << 16.
+struct LightDev { float ambient[3], sun[3], sun_dir[3]; uint32_t sky; };
 struct Chunk {                    // <= 256 triangles of one instance + their object-space AABB
   uint32_t inst, start, count, pad;
   float lo[3], hi[3];
@@ -60,13 +64,10 @@ struct SceneDev {
   const float* tri_pos;        // [T][3][3] object space
   const float* tri_uv;         // [T][3][2] (zeros for meshes without uvs)
   const InstDesc* inst;        // [I]
-  const MatDesc* mats;
   const TexDesc* texd;
   const uint8_t* texels;        // RGBA8, all textures back to back (TexDesc.offset in texels)
   const uint32_t* aquad;        // alpha quads, same indexing (see tex_alpha)
   uint32_t n_inst;
-  float ambient[3], sun[3], sun_dir[3];
-  uint32_t sky;                // packed r | g<<8 | b<<16
   uint32_t W, H, tiles_x, tiles_y, n_tiles;
   float near_clip, far_clip;
 };
@@ -74,6 +75,9 @@ struct SceneDev {
 struct BatchDev {
   const FrameDev* frames;      // [F]
   const float* models;         // [n_sets][I][16]
+  const MatDesc* mats;         // [n_sets][n_mat] materials with the set's texture swaps applied
+  const LightDev* lights;      // [n_sets]
+  uint32_t n_mat;
   float* clip;                 // [F][I][12] rows 0,1,3 of P*V*M
   float* pv;                   // [F][12]    rows 0,1,3 of P*V
   Rec* recs;                   // [F][rec_cap]

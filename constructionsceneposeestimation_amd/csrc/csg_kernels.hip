@@ -397,7 +397,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     if (!(on | of | ol | orr | ot | ob)) {
       hom_setup(v, h);
       if (h.ok) {
-        const MatDesc mat = s.mats[m.material];
+        const MatDesc mat = b.mats[(size_t)b.frames[f].xform_set * b.n_mat + m.material];
         float uv[6] = {0, 0, 0, 0, 0, 0};
         if (mat.alpha_test && m.has_uv) {
           const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
@@ -887,7 +887,9 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   for (int z = 0; z < 3; ++z) { e.A[z] = h.A[z]; e.B[z] = h.B[z]; e.C[z] = h.C[z]; }
   e.invdet = h.invdet;
   e.label = m.label;
-  const MatDesc mat = s.mats[m.material];
+  const uint32_t set = b.frames[f].xform_set;
+  const MatDesc mat = b.mats[(size_t)set * b.n_mat + m.material];
+  const LightDev& L = b.lights[set];
   e.tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
   e.base = (uint32_t)mat.base[0] | ((uint32_t)mat.base[1] << 8) | ((uint32_t)mat.base[2] << 16);
   const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
@@ -911,7 +913,7 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   e.n2 = 0;
   if (nn > 0.0f) {
     const float len = sqrtf(nn);
-    const float d = (nx * s.sun_dir[0] + ny * s.sun_dir[1]) + nz * s.sun_dir[2];
+    const float d = (nx * L.sun_dir[0] + ny * L.sun_dir[1]) + nz * L.sun_dir[2];
     cs = fabsf(d / len);
     // two-sided: the clip-space determinant is negative exactly when the face
     // normal points toward the camera (pixel projection with fx*fy > 0)
@@ -922,7 +924,7 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   uint32_t q[3];
 #pragma unroll
   for (int z = 0; z < 3; ++z) {
-    const float shade = s.ambient[z] + s.sun[z] * cs;
+    const float shade = L.ambient[z] + L.sun[z] * cs;
     const int qq = (int)(shade * 256.0f + 0.5f);
     q[z] = (uint32_t)min(max(qq, 0), 65535);
   }
@@ -1053,6 +1055,7 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
   }
   __syncthreads();
   const size_t npx = (size_t)s.W * s.H;
+  const uint32_t sky = b.lights[b.frames[f].xform_set].sky & 0xFFFFFFu;
   if (row_ok) {
     uint32_t rgb[4];
     int32_t ids[4];
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
       const int px = ox + lx0 + k;
       nrm[k][0] = nrm[k][1] = 0;
       if (key[k] == kEmptyKey) {
-        rgb[k] = s.sky & 0xFFFFFFu;
+        rgb[k] = sky;
         ids[k] = -1;
         dep[k] = INFINITY;
       } else if (slot[k] >= 0) {

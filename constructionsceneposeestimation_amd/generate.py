@@ -79,6 +79,9 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             st = wl.epoch(e)
             r.set_instance_transforms(k, st.models)
             r.set_keypoints(k, st.keypoints)
+            if st.dr is not None:
+                r.set_dr_light(k, st.dr.light)
+                r.set_dr_textures(k, st.dr.textures)
             set_of[e] = k
             if e not in pose_cache:
                 pose_cache[e] = object_poses(wl.scene, st.object_frames)

@@ -37,6 +37,16 @@ def make_frames(views: np.ndarray, projs: np.ndarray, sets: Sequence[int], frame
     return fr
 
 
+def _light_struct(light) -> "_lib.Light":
+    amb, sun, d, sky = light_constants(light)
+    L = _lib.Light()
+    L.ambient[:] = [float(x) for x in amb]
+    L.sun[:] = [float(x) for x in sun]
+    L.sun_dir[:] = [float(x) for x in d]
+    L.sky[:] = [int(x) for x in sky]
+    return L
+
+
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, max_frames: int = 8, device: int = 0,
                  intrinsics: Optional[Intrinsics] = None, records_per_frame: int = 0, bins_per_frame: int = 0):
@@ -118,13 +128,17 @@ class Renderer:
             a = np.ascontiguousarray(t.rgba, np.uint8)
             self._check(self.lib.csg_upload_texture(self.ctx, k, a.ctypes.data, a.shape[1], a.shape[0]),
                         "upload_texture")
-        amb, sun, d, sky = light_constants(self.scene.light)
-        L = _lib.Light()
-        L.ambient[:] = [float(x) for x in amb]
-        L.sun[:] = [float(x) for x in sun]
-        L.sun_dir[:] = [float(x) for x in d]
-        L.sky[:] = [int(x) for x in sky]
-        self._check(self.lib.csg_set_light(self.ctx, C.byref(L)), "set_light")
+        self._check(self.lib.csg_set_light(self.ctx, C.byref(_light_struct(self.scene.light))), "set_light")
+
+    def set_dr_light(self, set_id: int, light) -> None:
+        """Lighting of transform set ``set_id`` (a ``scene.model.Light``; C4 DR)."""
+        self._check(self.lib.csg_set_dr_light(self.ctx, set_id, C.byref(_light_struct(light))), "set_dr_light")
+
+    def set_dr_textures(self, set_id: int, texture_per_material) -> None:
+        """Texture of each material for transform set ``set_id``: an index into
+        ``scene.textures``, -1 for none, or ``_lib.KEEP_TEXTURE``."""
+        t = np.ascontiguousarray(np.asarray(texture_per_material, np.int32))
+        self._check(self.lib.csg_set_dr_textures(self.ctx, set_id, t.ctypes.data, t.shape[0]), "set_dr_textures")
 
     def set_instance_transforms(self, set_id: int, models: np.ndarray) -> None:
         m = np.ascontiguousarray(np.asarray(models, np.float64).reshape(-1, 16).astype(np.float32))

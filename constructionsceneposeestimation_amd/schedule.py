@@ -21,7 +21,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from .scene import xform as X
-from .scene.model import Scene
+from .scene.model import Light, Scene, Texture
 
 HEIGHTS = [1.6, 1.7, 1.8, 2.0, 2.5, 3.0]                         # :790
 DUMPER_CENTER = (-7.37, -0.59)                                  # :794
@@ -44,7 +44,7 @@ FENCE_X = (-9.0, 8.5)                                           # :935
 FENCE_Y = (-9.0, 9.0)                                           # :936
 DUMPER_AREAS = [(-7, -1), (-3, -5), (5, 0), (-5, 5), (3, -4), (6, 3), (-6, -4)]   # :1110-1118
 
-STREAM_CAMERA_RING, STREAM_CAMERA_RANDOM, STREAM_LAYOUT, STREAM_POSE = 1, 2, 3, 4
+STREAM_CAMERA_RING, STREAM_CAMERA_RANDOM, STREAM_LAYOUT, STREAM_POSE, STREAM_DR = 1, 2, 3, 4, 5
 
 
 def rng_for(seed: int, stream: int, index: int) -> np.random.Generator:
@@ -225,3 +225,71 @@ def object_frames_for_epoch(scene: Scene, seed: int, epoch: int) -> List[np.ndar
     for j, p in randomize_object_positions(scene, seed, epoch).items():
         frames[j] = placed_frame(frames[j], p)
     return frames
+
+
+# ---------------------------------------------------------------------------
+# Domain randomisation of lighting and textures (C4 of BASELINE.json)
+# ---------------------------------------------------------------------------
+# The reference fixes its lighting once (setup_scene_lighting,
+# generate_construction_data.py:1289-1345: dome 500, distant light clamped to
+# 1500) and never swaps textures; C4 adds per-epoch DR on top of the layout
+# randomisation, drawn from its own counter-based stream so it never perturbs
+# the layout or camera draws.
+KEEP_TEXTURE = -2
+DR_TINTS = {"autumn": (1.25, 0.85, 0.45), "dry": (1.05, 1.0, 0.7)}
+
+
+@dataclass
+class DRParams:
+    light: Light
+    textures: List[int]          # per material: texture index, -1 none, KEEP_TEXTURE
+
+
+def add_dr_texture_variants(scene: Scene) -> Dict[int, List[int]]:
+    """Append tinted copies of every material texture (alpha kept, so cut-out
+    silhouettes stay put) and return {material: [variant texture ids]}.
+    Idempotent: a second call returns the recorded variants."""
+    if "dr_variants" in scene.meta:
+        return {int(k): v for k, v in scene.meta["dr_variants"].items()}
+    made: Dict[int, List[int]] = {}
+    out: Dict[int, List[int]] = {}
+    for m, mat in enumerate(scene.materials):
+        if mat.texture < 0:
+            continue
+        if mat.texture not in made:
+            base = scene.textures[mat.texture].rgba
+            ids = []
+            for name, tint in DR_TINTS.items():
+                rgba = base.copy()
+                rgba[..., :3] = np.clip(np.round(base[..., :3].astype(np.float64) * np.asarray(tint)), 0, 255)
+                scene.textures.append(Texture(f"{scene.textures[mat.texture].name}:{name}", rgba.astype(np.uint8)))
+                ids.append(len(scene.textures) - 1)
+            made[mat.texture] = ids
+        out[m] = made[mat.texture]
+    scene.meta["dr_variants"] = {str(k): v for k, v in out.items()}
+    return out
+
+
+def domain_randomization(scene: Scene, seed: int, epoch: int, variants: Dict[int, List[int]]) -> DRParams:
+    """Lighting + texture choice of one epoch (epoch 0 = authored).  Dome tint
+    x U(0.8, 1.2) per channel, dome intensity 500 x U(0.6, 1.4), sun elevation
+    U(20, 75) deg, azimuth U(0, 360) deg, sun intensity U(750, 1500) (the
+    reference's 1500 clamp), each textured material picks its own texture or
+    one of its tinted variants uniformly."""
+    base = scene.light
+    if epoch == 0:
+        return DRParams(base, [KEEP_TEXTURE] * len(scene.materials))
+    rng = rng_for(seed, STREAM_DR, epoch)
+    dome = np.clip(np.asarray(base.dome_color, np.float64) * rng.uniform(0.8, 1.2, 3), 0.0, 1.0)
+    dome_i = float(base.dome_intensity) * float(rng.uniform(0.6, 1.4))
+    el = math.radians(float(rng.uniform(20.0, 75.0)))
+    az = math.radians(float(rng.uniform(0.0, 360.0)))
+    sun_dir = np.array([math.cos(el) * math.cos(az), math.cos(el) * math.sin(az), math.sin(el)])
+    sun_i = float(rng.uniform(750.0, 1500.0))
+    light = Light(sun_dir=sun_dir, sun_intensity=sun_i, sun_color=np.asarray(base.sun_color, np.float64),
+                  dome_intensity=dome_i, dome_color=dome)
+    tex = [KEEP_TEXTURE] * len(scene.materials)
+    for m in sorted(variants):
+        k = int(rng.integers(0, len(variants[m]) + 1))
+        tex[m] = KEEP_TEXTURE if k == 0 else variants[m][k - 1]
+    return DRParams(light, tex)

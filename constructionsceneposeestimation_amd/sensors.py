@@ -169,6 +169,9 @@ class Camera:
             r.set_instance_transforms(0, st.models)
             if st.keypoints.shape[0]:
                 r.set_keypoints(0, st.keypoints)
+            if st.dr is not None:
+                r.set_dr_light(0, st.dr.light)
+                r.set_dr_textures(0, st.dr.textures)
             self._uploaded_version = self.stage.version
         V, P, C = cm.frame_matrices(self._pos, self._quat, self.intrinsics())
         fr = make_frames(V[None], P[None], [0], [self._frame_id])

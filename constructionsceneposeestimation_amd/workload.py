@@ -9,7 +9,9 @@ can be produced by any process independently.
 * C2  world2 static (stands in for the missing world1.usd), 1920x1080
 * C3  world2 + crane/dumper/4 rigged-human proxies, 1920x1080, RGB + instance
       segmentation + 2D keypoints (the bench workload)
-* C4  C3 with per-epoch randomisation, frames seed-sharded across GPUs
+* C4  C3 with per-epoch DR of lighting (dome tint/intensity, sun) and
+      textures (tinted variants) on top of the layout randomisation, frames
+      seed-sharded across GPUs
 * C5  C3 at 3840x2160 with depth, normals (f16) and world points
 """
 from __future__ import annotations
@@ -30,7 +32,7 @@ WORKLOADS = {
     "C1": dict(scene="cone", width=256, height=256, outputs=("rgb", "instance", "depth")),
     "C2": dict(scene="world2", width=1920, height=1080, outputs=("rgb", "instance")),
     "C3": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints")),
-    "C4": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints")),
+    "C4": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints"), dr=True),
     "C5": dict(scene="world2_people", width=3840, height=2160,
                outputs=("rgb", "instance", "depth", "normals", "points", "keypoints")),
 }
@@ -60,6 +62,7 @@ class EpochState:
     object_frames: List[np.ndarray]    # per object
     keypoints: np.ndarray              # (K,3) world
     joints: Dict[int, Dict[str, np.ndarray]] = field(default_factory=dict)
+    dr: Optional["schedule.DRParams"] = None   # lighting / texture DR (C4), None = authored
 
 
 class Workload:
@@ -71,6 +74,8 @@ class Workload:
         self.height = int(height or spec["height"])
         self.outputs = spec["outputs"]
         self.scene = scene if scene is not None else build_scene(spec["scene"], n_humans)
+        self.dr = bool(spec.get("dr", False))
+        self.dr_variants = schedule.add_dr_texture_variants(self.scene) if self.dr else {}
         self.intr = cm.Intrinsics(self.width, self.height)
         self.base_models = np.stack([i.model for i in self.scene.instances])
         self.frames0 = [schedule.object_frame(self.scene, j) for j in range(len(self.scene.objects))]
@@ -122,6 +127,8 @@ class Workload:
             J = joints[j]
             kps.append(X.transform_points(frames[j], np.stack([J[n] for n in COCO_JOINTS])))
         st = EpochState(models, frames, np.vstack(kps) if kps else np.zeros((0, 3)), joints)
+        if self.dr:
+            st.dr = schedule.domain_randomization(self.scene, self.seed, e, self.dr_variants)
         self._epoch_cache[e] = st
         return st
 

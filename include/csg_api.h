@@ -16,6 +16,8 @@
  *                               distant light clamped to 1500)        :1289-1345
  *   csg_set_instance_transforms randomize_object_positions' xformOp
  *                               edits (every 10 frames)               :914-1231, :1542
+ *   csg_set_dr_light / ........ per-epoch domain randomisation (dome tint,
+ *   csg_set_dr_textures         sun, texture swap; C4 of BASELINE.json)
  *   csg_set_keypoints ......... (new) 3D points whose 2D projection is
  *                               annotated; the reference produces none
  *   csg_render_batch .......... camera.set_world_pose + next_update_async
@@ -38,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 2
+#define CSG_ABI_VERSION 3
 
 typedef enum {
   CSG_OK = 0,
@@ -136,6 +138,15 @@ int csg_set_light(csg_ctx* ctx, const csg_light* light);
 int csg_set_instance_transforms(csg_ctx* ctx, uint32_t set_id, const float* model4x4, uint32_t n);
 /* World-space keypoints of one transform set: [n][3]; n is fixed per scene. */
 int csg_set_keypoints(csg_ctx* ctx, uint32_t set_id, const float* pts_world, uint32_t n);
+
+/* Domain randomisation per transform set (randomisation epoch; C4).
+ * csg_set_dr_light: the set's lighting (dome tint/intensity, sun), replacing
+ * the csg_set_light default for frames of that set.
+ * csg_set_dr_textures: per material, the texture the set uses: a texture id,
+ * -1 for none, or CSG_KEEP_TEXTURE for the material's own; n = n_materials. */
+#define CSG_KEEP_TEXTURE (-2)
+int csg_set_dr_light(csg_ctx* ctx, uint32_t set_id, const csg_light* light);
+int csg_set_dr_textures(csg_ctx* ctx, uint32_t set_id, const int32_t* texture_per_material, uint32_t n);
 
 /* Render n_frames (<= max_frames) frames; synchronous. */
 int csg_render_batch(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out);

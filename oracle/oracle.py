@@ -109,6 +109,24 @@ class Oracle:
         s.near_clip, s.far_clip = near, far
         self.s = s
 
+    def set_light(self, light) -> None:
+        """Lighting for the following renders (a ``scene.model.Light``)."""
+        from constructionsceneposeestimation_amd.packing import light_constants
+        amb, sun, d, sky = light_constants(light)
+        self.s.ambient[:] = [float(x) for x in amb]
+        self.s.sun[:] = [float(x) for x in sun]
+        self.s.sun_dir[:] = [float(x) for x in d]
+        self.s.sky[:] = [int(x) for x in sky]
+
+    def set_material_textures(self, texture_per_material) -> None:
+        """Texture of each material for the following renders (-2 = keep)."""
+        mats = np.array(self.p.materials, copy=True)
+        for m, t in enumerate(texture_per_material):
+            if int(t) != -2:
+                mats["texture"][m] = int(t)
+        self._keep.append(mats)
+        self.s.materials = mats.ctypes.data
+
     def set_instance_models(self, models16: np.ndarray) -> None:
         a = np.ascontiguousarray(models16, np.float32).reshape(-1, 16)
         assert a.shape[0] == self.s.n_inst

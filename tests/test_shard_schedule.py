@@ -121,3 +121,33 @@ def test_two_rank_gloo_union_equals_single_process(tmp_path):
         v, p = wl.frame_params([f])
         r = o.render(v[0], p[0])
         assert union[f] == (r["rgb"].tobytes(), r["instance"].tobytes())
+
+
+def test_domain_randomization_is_keyed_and_bounded(world2):
+    import copy
+    from constructionsceneposeestimation_amd import schedule
+    sc = copy.deepcopy(world2)
+    n_tex = len(sc.textures)
+    var = schedule.add_dr_texture_variants(sc)
+    assert var and len(sc.textures) == n_tex + 2 * len({sc.materials[m].texture for m in var})
+    assert schedule.add_dr_texture_variants(sc) == var and len(sc.textures) == n_tex + 2 * len(
+        {sc.materials[m].texture for m in var})
+    for m, ids in var.items():
+        base = sc.textures[sc.materials[m].texture].rgba
+        for t in ids:   # tinted copies keep the alpha channel (cut-outs unchanged)
+            assert np.array_equal(sc.textures[t].rgba[..., 3], base[..., 3])
+    p0 = schedule.domain_randomization(sc, 7, 0, var)
+    assert p0.light is sc.light and all(t == schedule.KEEP_TEXTURE for t in p0.textures)
+    seen = set()
+    for e in range(1, 40):
+        a = schedule.domain_randomization(sc, 7, e, var)
+        b = schedule.domain_randomization(sc, 7, e, var)
+        assert np.array_equal(a.light.sun_dir, b.light.sun_dir) and a.textures == b.textures
+        assert 750.0 <= a.light.sun_intensity <= 1500.0 and 300.0 <= a.light.dome_intensity <= 700.0
+        assert abs(np.linalg.norm(a.light.sun_dir) - 1.0) < 1e-12 and a.light.sun_dir[2] > 0.3
+        for m, t in enumerate(a.textures):
+            assert t == schedule.KEEP_TEXTURE or t in var[m]
+        seen.add(tuple(a.textures))
+    assert len(seen) > 1
+    c = schedule.domain_randomization(sc, 8, 5, var)
+    assert not np.array_equal(c.light.sun_dir, schedule.domain_randomization(sc, 7, 5, var).light.sun_dir)
