@@ -11,7 +11,7 @@ from typing import Optional
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 3  # CSG_ABI_VERSION in include/csg_api.h
+ABI_VERSION = 4  # CSG_ABI_VERSION in include/csg_api.h
 KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
 
 EXPORTED = (
@@ -19,6 +19,7 @@ EXPORTED = (
     "csg_upload_texture", "csg_set_light", "csg_set_instance_transforms", "csg_set_keypoints",
     "csg_render_batch", "csg_render_batch_async", "csg_synchronize", "csg_get_batch_stats",
     "csg_project_keypoints", "csg_timing_reset", "csg_timing_read", "csg_set_dr_light", "csg_set_dr_textures",
+    "csg_instance_bounds",
 )
 
 
@@ -116,6 +117,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib.csg_timing_read.argtypes = [vp, C.POINTER(Timing)]
     lib.csg_set_dr_light.argtypes = [vp, u32, C.POINTER(Light)]
     lib.csg_set_dr_textures.argtypes = [vp, u32, vp, u32]
+    lib.csg_instance_bounds.argtypes = [vp, u32, vp]
     if lib.csg_abi_version() != ABI_VERSION:
         raise CsgError(f"libcsg.so ABI {lib.csg_abi_version()} != binding ABI {ABI_VERSION}; rebuild")
     _lib = lib

@@ -9,9 +9,11 @@ build's additions.
   "idToSemantics"}}`` (:1818-1842); id 0 = background/unlabelled, id k+1 =
   object ``inst_idx`` k;
 * ``bounding_box_3d`` -> ``{"data": structured records (semanticId, x/y/z
-  min/max, 4x4 transform, occlusionRatio), "info": {"primPaths"}}`` for the
-  objects visible in the frame (:1780-1790, :1916-1922, read positionally by
-  ``bboxDict_to_transform`` :562-564);
+  min/max, 4x4 transform, occlusionRatio), "info": {"primPaths",
+  "worldBounds"}}`` for the objects visible in the frame (:1780-1790,
+  :1916-1922, read positionally by ``bboxDict_to_transform`` :562-564);
+  ``worldBounds`` (N,2,3) is the world AABB of each object's vertices,
+  reduced on the GPU;
 * ``pointcloud`` -> ``{"data": (N,3) float32 world points, "pointRgb": (N,4)
   uint8, "info": {...}}`` (:1614, :1720-1724, :735);
 * ``normals`` -> H x W x 3 float16 unit world-space normals facing the camera
@@ -88,7 +90,8 @@ class Annotator:
             if self.name == "bounding_box_3d":
                 recs = bbox3d_records(scene, cam.stage.state.object_frames)
                 return {"data": recs[vis], "info": {"primPaths": [scene.objects[j].prim_path for j in vis],
-                                                     "idToLabels": {j: scene.objects[j].class_name for j in vis}}}
+                                                     "idToLabels": {j: scene.objects[j].class_name for j in vis},
+                                                     "worldBounds": cam.object_world_bounds()[vis]}}
             dt = np.dtype([("semanticId", "<u4"), ("x_min", "<i4"), ("y_min", "<i4"), ("x_max", "<i4"),
                            ("y_max", "<i4"), ("pixelCount", "<u4")])
             rec = np.zeros(len(vis), dt)

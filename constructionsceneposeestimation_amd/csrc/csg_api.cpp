@@ -773,4 +773,33 @@ int csg_project_keypoints(csg_ctx* c, const float* pts, uint32_t n, const float*
   return CSG_OK;
 }
 
+int csg_instance_bounds(csg_ctx* c, uint32_t set_id, float* out) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!out) return c->fail(CSG_ERR_INVALID, "instance_bounds: null output");
+  if (set_id >= c->set_valid.size() || !c->set_valid[set_id])
+    return c->fail(CSG_ERR_INVALID, "instance_bounds: transform set %u not uploaded", set_id);
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const int rc = sync_scene_state(c);
+  if (rc) return rc;
+  const size_t n = (size_t)c->n_inst * 6;
+  // ordered-uint encoding: min slots start at max, max slots at 0
+  std::vector<uint32_t> init(n);
+  for (size_t k = 0; k < n; ++k) init[k] = (k % 6) < 3 ? 0xFFFFFFFFu : 0u;
+  DevBuf<uint32_t> d;
+  HIP_TRY(c, d.alloc(n));
+  HIP_TRY(c, hipMemcpy(d.p, init.data(), n * 4, hipMemcpyHostToDevice));
+  launch_inst_bounds(scene_dev(c), c->chunks.p, c->n_chunks, c->models.p + (size_t)set_id * c->n_inst * 16, d.p,
+                     c->stream);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(init.data(), d.p, n * 4, hipMemcpyDeviceToHost));
+  d.release();
+  for (size_t k = 0; k < n; ++k) {
+    const uint32_t o = init[k];
+    const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    memcpy(&out[k], &u, 4);
+  }
+  return CSG_OK;
+}
+
 }  // extern "C"

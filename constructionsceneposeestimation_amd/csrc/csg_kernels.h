@@ -120,6 +120,8 @@ void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st, int variant);
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_inst_bounds(const SceneDev& s, const Chunk* chunks, uint32_t n_chunks, const float* models,
+                        uint32_t* out, hipStream_t st);
 void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip,
                     float* uv, int32_t* vis, hipStream_t st);
 

@@ -1227,6 +1227,56 @@ __global__ __launch_bounds__(256) void k_keypoints(SceneDev s, BatchDev b) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_inst_bounds: world-space AABB of every instance's vertices under one
+// transform set (3D bbox annotator, GDP:1780-1790).  One block per chunk;
+// wave min/max, then order-preserving uint atomics (decoded on the host).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ordered_bits(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(256) void k_inst_bounds(SceneDev s, const Chunk* __restrict__ chunks,
+                                                     const float* __restrict__ models, uint32_t* __restrict__ out) {
+  const Chunk ch = chunks[blockIdx.x];
+  const int tid = threadIdx.x;
+  const uint32_t i = ch.inst;
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  if ((uint32_t)tid < ch.count) {
+    const float* M = models + (size_t)i * 16;
+    float m[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) m[k] = M[k];
+    const float* tp = s.tri_pos + (size_t)(s.inst[i].tbase + ch.start + tid) * 9;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      const float x = tp[3 * v], y = tp[3 * v + 1], z = tp[3 * v + 2];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const float w = dot4(m + 4 * a, x, y, z);
+        lo[a] = fminf(lo[a], w);
+        hi[a] = fmaxf(hi[a], w);
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      lo[a] = fminf(lo[a], __shfl_xor(lo[a], d, 64));
+      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], d, 64));
+    }
+  }
+  if ((tid & 63) == 0 && (uint32_t)tid < ch.count) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(&out[i * 6 + a], ordered_bits(lo[a]));
+      atomicMax(&out[i * 6 + 3 + a], ordered_bits(hi[a]));
+    }
+  }
+}
+
 __global__ void k_project(const float* pts, uint32_t n, const float* pv, float Wf, float Hf, float nearc, float* uv,
                           int32_t* vis) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1284,6 +1334,11 @@ void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStrea
   if (!b.n_kp) return;
   dim3 g((b.n_kp + 255) / 256, F);
   hipLaunchKernelGGL(k_keypoints, g, dim3(256), 0, st, s, b);
+}
+
+void launch_inst_bounds(const SceneDev& s, const Chunk* chunks, uint32_t n_chunks, const float* models,
+                        uint32_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_inst_bounds, dim3(n_chunks), dim3(kBlock), 0, st, s, chunks, models, out);
 }
 
 void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip, float* uv,

@@ -196,6 +196,12 @@ class Renderer:
         self._check(self.lib.csg_render_batch_async(self.ctx, frames_ptr, n, int(frames_on_device), C.byref(o),
                                                     stream or None), "render_batch_async")
 
+    def instance_bounds(self, set_id: int = 0) -> np.ndarray:
+        """(I, 2, 3) float32 world-space AABB of every instance under a transform set (GPU reduction)."""
+        out = np.empty((self.n_inst, 6), np.float32)
+        self._check(self.lib.csg_instance_bounds(self.ctx, set_id, out.ctypes.data), "instance_bounds")
+        return out.reshape(-1, 2, 3)
+
     def synchronize(self) -> None:
         self._check(self.lib.csg_synchronize(self.ctx), "synchronize")
 

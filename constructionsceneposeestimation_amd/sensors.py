@@ -161,7 +161,8 @@ class Camera:
         return cm.get_obj_pose_from_matrix(cm.camera_usd_transform(self._pos, self._quat))
 
     # -- rendering (called from next_update) ----------------------------------
-    def _render(self) -> None:
+    def _sync_stage(self) -> None:
+        """Upload the stage's current epoch (transforms, keypoints, DR) if it changed."""
         self.initialize()
         r = self._renderer
         if self._uploaded_version != self.stage.version:
@@ -173,6 +174,10 @@ class Camera:
                 r.set_dr_light(0, st.dr.light)
                 r.set_dr_textures(0, st.dr.textures)
             self._uploaded_version = self.stage.version
+
+    def _render(self) -> None:
+        self._sync_stage()
+        r = self._renderer
         V, P, C = cm.frame_matrices(self._pos, self._quat, self.intrinsics())
         fr = make_frames(V[None], P[None], [0], [self._frame_id])
         out = r.render(fr, want=("rgb", "instance", "depth", "keypoints", "stats") + tuple(sorted(self._extra)))
@@ -181,6 +186,22 @@ class Camera:
                             "frame_id": self._frame_id}
         self._frame_id += 1
         self._dirty = False
+
+    def object_world_bounds(self) -> np.ndarray:
+        """(n_objects, 2, 3) world AABB of each labelled object's vertices in
+        the current epoch (GPU reduction over its instances; NaN if none)."""
+        self._sync_stage()
+        if getattr(self, "_bounds_version", None) != self.stage.version:
+            ib = self._renderer.instance_bounds(0)
+            ob = np.full((len(self.stage.scene.objects), 2, 3), np.nan, np.float32)
+            for i, inst in enumerate(self.stage.scene.instances):
+                j = inst.obj
+                if j < 0 or not np.all(np.isfinite(ib[i])):
+                    continue
+                ob[j, 0] = np.fmin(ob[j, 0], ib[i, 0])
+                ob[j, 1] = np.fmax(ob[j, 1], ib[i, 1])
+            self._bounds, self._bounds_version = ob, self.stage.version
+        return self._bounds
 
     def get_rgba(self) -> Optional[np.ndarray]:
         if self._frame is None:

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 3
+#define CSG_ABI_VERSION 4
 
 typedef enum {
   CSG_OK = 0,
@@ -169,6 +169,11 @@ typedef struct {
 } csg_timing;
 int csg_timing_reset(csg_ctx* ctx);
 int csg_timing_read(csg_ctx* ctx, csg_timing* out);
+
+/* World-space AABB of each instance's vertices under transform set set_id,
+ * out [n_instances][6] = xmin, ymin, zmin, xmax, ymax, zmax (host buffer);
+ * the GPU side of the bounding_box_3d annotator (GDP:1780-1790). */
+int csg_instance_bounds(csg_ctx* ctx, uint32_t set_id, float* out);
 
 /* Stand-alone 3D->2D projection (host buffers): uv [n][2], vis [n] without a
  * depth test (1 = in front and inside the image, 0 otherwise). */

@@ -59,9 +59,12 @@ def test_camera_annotator_loop_matches_oracle(stage):
         assert set(inst["info"]["idToLabels"]) == set(np.unique(ids[ids > 0]).tolist())
         # bbox_3d records are consumable by the reference's own conversion
         assert len(boxes["info"]["primPaths"]) == len(boxes["data"]) > 0
-        for rec in boxes["data"]:
+        wb = boxes["info"]["worldBounds"]
+        assert wb.shape == (len(boxes["data"]), 2, 3)
+        for rec, b in zip(boxes["data"], wb):
             c, s, e = bboxDict_to_transform(tuple(rec))
             assert all(np.isfinite(c)) and all(x >= 0 for x in s)
+            assert np.all(b[0] <= b[1])
         # point cloud: one point per finite depth pixel, on the camera ray
         assert pcd["data"].shape == (int(np.isfinite(depth).sum()), 3)
         fin = np.isfinite(ref["depth"])
