@@ -1,8 +1,9 @@
-"""Build libcsg.so (HIP, gfx950) in-tree with hipcc.
+"""Build libcsg.so (HIP, gfx950) with hipcc and libcsgio.so (host writers)
+with g++, both in-tree.
 
 ``python -m constructionsceneposeestimation_amd.build`` — cross-compiles
-without a GPU.  The .so is git-ignored but travels to the GPU box with the
-repo snapshot.
+without a GPU.  The .so files are git-ignored but travel to the GPU box with
+the repo snapshot.
 """
 from __future__ import annotations
 
@@ -17,6 +18,10 @@ LIB = os.path.join(PKG, "libcsg.so")
 SOURCES = [os.path.join(PKG, "csrc", "csg_kernels.hip"), os.path.join(PKG, "csrc", "csg_api.cpp")]
 DEPS = SOURCES + [os.path.join(PKG, "csrc", "csg_kernels.h"), os.path.join(ROOT, "include", "csg_api.h")]
 ARCH = os.environ.get("CSG_OFFLOAD_ARCH", "gfx950")
+IO_LIB = os.path.join(PKG, "libcsgio.so")
+IO_SOURCES = [os.path.join(PKG, "csrc", "csg_io.cpp")]
+IO_DEPS = IO_SOURCES + [os.path.join(ROOT, "include", "csg_io.h")]
+IO_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread"]
 
 # -ffp-contract=off: the raster spec's float expressions must round exactly as
 # written (bit-exact with the CPU oracle).  HIP keeps fp32 '/' and sqrtf
@@ -31,11 +36,12 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm required to build libcsg.so)")
 
 
-def needs_build() -> bool:
-    if not os.path.exists(LIB):
+def needs_build(lib: str = LIB, deps=None) -> bool:
+    deps = DEPS if deps is None else deps
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in DEPS)
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(p) > t for p in deps)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -48,5 +54,17 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_io(force: bool = False, verbose: bool = False) -> str:
+    if force or needs_build(IO_LIB, IO_DEPS):
+        cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+        cmd = [cxx, *IO_FLAGS, "-o", IO_LIB + ".tmp", *IO_SOURCES, "-lz"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(IO_LIB + ".tmp", IO_LIB)
+    return IO_LIB
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_io(force="--force" in sys.argv, verbose=True))

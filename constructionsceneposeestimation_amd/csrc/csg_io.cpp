@@ -1,0 +1,175 @@
+// libcsgio.so: host-side writers of the generator's on-disk formats
+// (include/csg_io.h).  Each call writes one file; no shared state, so the
+// Python generator runs a pool of threads through ctypes (which releases the
+// GIL) while the GPU renders the next batch.
+#include "../../include/csg_io.h"
+
+#include <zlib.h>
+
+#include <cerrno>
+#include <charconv>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct File {
+  FILE* f = nullptr;
+  explicit File(const char* path) : f(path ? std::fopen(path, "wb") : nullptr) {}
+  ~File() {
+    if (f) std::fclose(f);
+  }
+  bool write(const void* p, size_t n) { return std::fwrite(p, 1, n, f) == n; }
+  int close() {
+    const int rc = std::fclose(f);
+    f = nullptr;
+    return rc == 0 ? 0 : -EIO;
+  }
+};
+
+void put_be32(std::vector<uint8_t>& v, uint32_t x) {
+  v.push_back((uint8_t)(x >> 24));
+  v.push_back((uint8_t)(x >> 16));
+  v.push_back((uint8_t)(x >> 8));
+  v.push_back((uint8_t)x);
+}
+
+void png_chunk(std::vector<uint8_t>& out, const char* type, const uint8_t* data, size_t n) {
+  put_be32(out, (uint32_t)n);
+  const size_t at = out.size();
+  out.insert(out.end(), type, type + 4);
+  if (n) out.insert(out.end(), data, data + n);
+  const uint32_t crc = (uint32_t)crc32(0L, out.data() + at, (uInt)(n + 4));
+  put_be32(out, crc);
+}
+
+// "%.6f" of a double, as printf in the C locale (std::to_chars is specified so).
+inline char* fmt6(char* p, char* end, double x) {
+  if (std::isnan(x)) {
+    if (std::signbit(x)) *p++ = '-';
+    std::memcpy(p, "nan", 3);
+    return p + 3;
+  }
+  return std::to_chars(p, end, x, std::chars_format::fixed, 6).ptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int csgio_abi_version(void) { return CSGIO_ABI_VERSION; }
+
+int csgio_write_png_rgb(const char* path, const uint8_t* rgb, uint32_t w, uint32_t h, int level) {
+  if (!path || !rgb || !w || !h || level < 0 || level > 9) return -EINVAL;
+  // filter type 1 (Sub) on every row: byte minus the byte one pixel to the left
+  const size_t stride = (size_t)w * 3;
+  std::vector<uint8_t> raw((stride + 1) * h);
+  for (uint32_t y = 0; y < h; ++y) {
+    uint8_t* d = &raw[(stride + 1) * y];
+    const uint8_t* s = rgb + stride * y;
+    d[0] = 1;
+    std::memcpy(d + 1, s, 3);
+    for (size_t x = 3; x < stride; ++x) d[1 + x] = (uint8_t)(s[x] - s[x - 3]);
+  }
+  uLongf zn = compressBound((uLong)raw.size());
+  std::vector<uint8_t> z(zn);
+  if (compress2(z.data(), &zn, raw.data(), (uLong)raw.size(), level) != Z_OK) return -EIO;
+  std::vector<uint8_t> out;
+  out.reserve(zn + 64);
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+  out.insert(out.end(), sig, sig + 8);
+  std::vector<uint8_t> ihdr;
+  put_be32(ihdr, w);
+  put_be32(ihdr, h);
+  ihdr.push_back(8);   // bit depth
+  ihdr.push_back(2);   // colour type RGB
+  ihdr.push_back(0);   // deflate
+  ihdr.push_back(0);   // adaptive filtering
+  ihdr.push_back(0);   // no interlace
+  png_chunk(out, "IHDR", ihdr.data(), ihdr.size());
+  png_chunk(out, "IDAT", z.data(), zn);
+  png_chunk(out, "IEND", nullptr, 0);
+  File f(path);
+  if (!f.f) return -errno;
+  if (!f.write(out.data(), out.size())) return -EIO;
+  return f.close();
+}
+
+int csgio_write_npy(const char* path, const void* data, uint64_t nbytes, const char* descr, const uint64_t* shape,
+                    uint32_t ndim) {
+  if (!path || (!data && nbytes) || !descr || (!shape && ndim)) return -EINVAL;
+  std::string dict = std::string("{'descr': '") + descr + "', 'fortran_order': False, 'shape': (";
+  for (uint32_t k = 0; k < ndim; ++k) {
+    dict += std::to_string(shape[k]);
+    if (ndim == 1 || k + 1 < ndim) dict += ",";
+    if (k + 1 < ndim) dict += " ";
+  }
+  dict += "), }";
+  // magic(6) + version(2) + header length(2) + dict + padding + '\n', total % 64 == 0
+  size_t total = 10 + dict.size() + 1;
+  const size_t pad = (64 - total % 64) % 64;
+  dict.append(pad, ' ');
+  dict += '\n';
+  const uint16_t hl = (uint16_t)dict.size();
+  File f(path);
+  if (!f.f) return -errno;
+  const uint8_t head[8] = {0x93, 'N', 'U', 'M', 'P', 'Y', 1, 0};
+  const uint8_t hlb[2] = {(uint8_t)(hl & 255u), (uint8_t)(hl >> 8)};
+  if (!f.write(head, 8) || !f.write(hlb, 2) || !f.write(dict.data(), dict.size())) return -EIO;
+  if (nbytes && !f.write(data, nbytes)) return -EIO;
+  return f.close();
+}
+
+int csgio_write_depth_csv(const char* path, const float* d, uint32_t w, uint32_t h) {
+  if (!path || !d || !w || !h) return -EINVAL;
+  File f(path);
+  if (!f.f) return -errno;
+  std::vector<char> line((size_t)w * 48 + 2);
+  for (uint32_t y = 0; y < h; ++y) {
+    char* p = line.data();
+    char* end = line.data() + line.size();
+    for (uint32_t x = 0; x < w; ++x) {
+      if (x) *p++ = ' ';
+      p = fmt6(p, end, (double)d[(size_t)y * w + x]);
+    }
+    *p++ = '\n';
+    if (!f.write(line.data(), (size_t)(p - line.data()))) return -EIO;
+  }
+  return f.close();
+}
+
+int csgio_write_pointcloud_txt(const char* path, const float* xyz, const uint8_t* rgb, uint64_t n) {
+  if (!path || (n && (!xyz || !rgb))) return -EINVAL;
+  File f(path);
+  if (!f.f) return -errno;
+  static const char head[] = "x y z r g b\n";
+  if (!f.write(head, sizeof(head) - 1)) return -EIO;
+  std::vector<char> buf(1 << 20);
+  size_t used = 0;
+  for (uint64_t k = 0; k < n; ++k) {
+    const float* p3 = xyz + 3 * k;
+    if (std::isnan(p3[0]) || std::isnan(p3[1]) || std::isnan(p3[2])) continue;
+    if (buf.size() - used < 6 * 48 + 2) {
+      if (!f.write(buf.data(), used)) return -EIO;
+      used = 0;
+    }
+    char* p = buf.data() + used;
+    char* end = buf.data() + buf.size();
+    for (int c = 0; c < 3; ++c) {
+      p = fmt6(p, end, (double)p3[c]);
+      *p++ = ' ';
+    }
+    for (int c = 0; c < 3; ++c) {
+      p = fmt6(p, end, (double)rgb[3 * k + c]);
+      *p++ = c < 2 ? ' ' : '\n';
+    }
+    used = (size_t)(p - buf.data());
+  }
+  if (used && !f.write(buf.data(), used)) return -EIO;
+  return f.close();
+}
+
+}  // extern "C"

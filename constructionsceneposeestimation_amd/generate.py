@@ -34,6 +34,7 @@ from typing import List, Optional
 import numpy as np
 
 from . import camera_math as cm
+from . import writers as fileio
 from .labels import label_record, object_poses, save_label_json
 from .quality_log import QualityLog
 from .renderer import Renderer, make_frames
@@ -42,16 +43,13 @@ from .workload import Workload
 
 
 def _write_png(path: str, rgb: np.ndarray) -> None:
-    from PIL import Image
-    Image.fromarray(rgb).save(path, compress_level=1)
+    fileio.write_png(path, rgb, level=1)
 
 
 def _write_pointcloud(path: str, points: np.ndarray, rgb: np.ndarray) -> None:
     """``x y z r g b`` per hit pixel (generate_construction_data.py:769-770);
     the world points come from the GPU resolve (NaN where nothing is hit)."""
-    m = np.isfinite(points[..., 0])
-    xyzrgb = np.hstack([points[m].astype(np.float64), rgb[m].astype(np.float64)])
-    np.savetxt(path, xyzrgb, fmt="%.6f", delimiter=" ", header="x y z r g b", comments="")
+    fileio.write_pointcloud_txt(path, points, rgb)
 
 
 def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 30,
@@ -94,22 +92,23 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                                wl.kp_table, wl.height, wl.width)
             log.frame(lab["num_objects"], out["depth"][k] if "depth" in out else None, out["keypoints_vis"][k])
             pending.append(pool.submit(_write_png, os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), out["rgb"][k]))
-            pending.append(pool.submit(np.save, os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"),
+            pending.append(pool.submit(fileio.write_npy,
+                                       os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"),
                                        out["instance"][k]))
             pending.append(pool.submit(save_label_json, lab, os.path.join(out_dir, "labels", f"label_{f:06d}.json")))
             if depth:
-                pending.append(pool.submit(np.save, os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"),
+                pending.append(pool.submit(fileio.write_npy, os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"),
                                            out["depth"][k]))
                 if depth_csv:
-                    pending.append(pool.submit(np.savetxt, os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"),
-                                               out["depth"][k], delimiter=" ", fmt="%.6f"))
+                    pending.append(pool.submit(fileio.write_depth_csv,
+                                               os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), out["depth"][k]))
             if pointcloud:
                 pending.append(pool.submit(_write_pointcloud, os.path.join(out_dir, "pointcloud",
                                                                            f"pointcloud_{f:06d}.txt"),
                                            out["points"][k], out["rgb"][k]))
             if normals:
-                pending.append(pool.submit(np.save, os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"),
-                                           out["normals"][k]))
+                pending.append(pool.submit(fileio.write_npy,
+                                           os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), out["normals"][k]))
         # bound the queue so host memory stays flat
         while len(pending) > 64 * max(writers, 1):
             pending.pop(0).result()
