@@ -120,6 +120,7 @@ struct csg_ctx {
   hipEvent_t* ev = nullptr;             // events of the most recent batch
   uint32_t last_F = 0;
   uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
+  uint32_t bin_blocks = 128;            // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only)
   int raster_variant = 0;               // k_raster expansion variant (CSG_VARIANT overrides; A/B only)
 
   int fail(int code, const char* fmt, ...) {
@@ -157,6 +158,7 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   c->cfg = *cfg;
   if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
   if (const char* v = getenv("CSG_VARIANT")) c->raster_variant = atoi(v);
+  if (const char* v = getenv("CSG_BINBLOCKS")) c->bin_blocks = std::max(1, std::min(1024, atoi(v)));
   c->tiles_x = (cfg->width + kTile - 1) / kTile;
   c->tiles_y = (cfg->height + kTile - 1) / kTile;
   c->n_tiles = c->tiles_x * c->tiles_y;
@@ -505,6 +507,7 @@ static SceneDev scene_dev(const csg_ctx* c) {
   s.W = c->cfg.width; s.H = c->cfg.height;
   s.tiles_x = c->tiles_x; s.tiles_y = c->tiles_y; s.n_tiles = c->n_tiles;
   s.near_clip = c->cfg.near_clip; s.far_clip = c->cfg.far_clip;
+  s.dbg = c->dbg;
   return s;
 }
 
@@ -610,9 +613,9 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   launch_clip(s, b, F, st);
   launch_setup(s, b, c->chunks.p, c->n_chunks, F, st);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
-  launch_count(s, b, F, st);
+  launch_count(s, b, F, c->bin_blocks, st);
   launch_scan(s, b, F, st);
-  launch_bin(s, b, F, st);
+  launch_bin(s, b, F, c->bin_blocks, st);
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
   launch_keypoints(s, b, F, st);   // projection; k_raster depth-tests against its z-buffer
   if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));

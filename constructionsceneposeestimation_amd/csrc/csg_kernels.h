@@ -70,6 +70,7 @@ struct SceneDev {
   uint32_t n_inst;
   uint32_t W, H, tiles_x, tiles_y, n_tiles;
   float near_clip, far_clip;
+  uint32_t dbg;                // ablation switches (CSG_DEBUG; 0 in production)
 };
 
 struct BatchDev {
@@ -114,9 +115,9 @@ struct BatchDev {
 void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks,
                   uint32_t F, hipStream_t st);
-void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
-void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st, int variant);
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);

@@ -98,8 +98,8 @@ __device__ __forceinline__ int wrap_index(float fu, int n) {
   const float nf = (float)n;
   const float q = floorf(fu * __builtin_amdgcn_rcpf(nf));
   float r = fu - q * nf;
-  if (r < 0.0f) r += nf;
-  else if (r >= nf) r -= nf;
+  r += r < 0.0f ? nf : 0.0f;
+  r -= r >= nf ? nf : 0.0f;
   return (int)r;
 }
 
@@ -336,13 +336,14 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63;
   if (b.dbg & 32u) return;            // ablation: empty setup
-  const Chunk ch = chunks[blockIdx.x];
+  const Chunk& ch = chunks[blockIdx.x];   // read fields in place (a runtime-indexed copy would spill)
   const uint32_t i = ch.inst;
   const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
   // Chunk cull: every wave evaluates the 8 corners of the chunk's object-space
   // AABB (lanes 0-7) and the block leaves if all corners fail one frustum
   // plane by a margin -- then every triangle inside would fail that plane in
-  // the per-triangle test too, so the output is unchanged.
+  // the per-triangle test too, so the output is unchanged.  (Measured: per-
+  // 64-triangle slice AABBs cull more but cost more than they save.)
   {
     bool out_n = true, out_f = true, out_l = true, out_r = true, out_t = true, out_b = true;
     const int cidx = lane & 7;
@@ -941,7 +942,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
   id_out = e.label;
   int base[3] = {(int)(e.base & 255u), (int)((e.base >> 8) & 255u), (int)((e.base >> 16) & 255u)};
   int alb[3];
-  if (e.tex >= 0) {
+  if (e.tex >= 0 && !(s.dbg & 4096u)) {   // 4096: ablation only, no texture fetch
     float u, v;
     int c[4];
     interp_uv(ev, ssum, e.uv, u, v);
@@ -1049,7 +1050,12 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
     const uint32_t u = L.q.keys[tid];
     if (u != kNoAlpha) {
       ShadeEntry e;
-      shade_setup(s, b, f, u, e);
+      if (b.dbg & 8192u) {   // ablation only: no triangle setup (garbage shading)
+        e = ShadeEntry{};
+        e.invdet = 1.0f; e.tex = -1; e.label = 0;
+      } else {
+        shade_setup(s, b, f, u, e);
+      }
       L.q.tab[tid] = e;
     }
   }
@@ -1239,7 +1245,7 @@ __device__ __forceinline__ uint32_t ordered_bits(float x) {
 
 __global__ __launch_bounds__(256) void k_inst_bounds(SceneDev s, const Chunk* __restrict__ chunks,
                                                      const float* __restrict__ models, uint32_t* __restrict__ out) {
-  const Chunk ch = chunks[blockIdx.x];
+  const Chunk& ch = chunks[blockIdx.x];
   const int tid = threadIdx.x;
   const uint32_t i = ch.inst;
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -1303,17 +1309,17 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
   hipLaunchKernelGGL(k_setup, g, dim3(kBlock), 0, st, s, b, chunks);
 }
 
-void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
   const size_t lds = (((s.n_tiles + 3u) & ~3u) + 3 * kBlock + 12) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_count, dim3(64, F), dim3(kBlock), lds, st, s, b);
+  hipLaunchKernelGGL(k_count, dim3(blocks, F), dim3(kBlock), lds, st, s, b);
 }
 
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
   hipLaunchKernelGGL(k_scan, dim3(F), dim3(kBlock), 0, st, s, b);
 }
 
-void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
-  dim3 g(64, F);
+void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
+  dim3 g(blocks, F);
   hipLaunchKernelGGL(k_bin, g, dim3(kBlock), 2 * s.n_tiles * sizeof(uint32_t), st, s, b);
 }
 
