@@ -46,8 +46,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames-per-step", type=int, default=60)
     ap.add_argument("--workload", default="C3")
+    ap.add_argument("--frames-per-launch", type=int, default=0, help="frames per kernel chain (0 = library default)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=96, help="frames rendered by the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=384, help="frames rendered by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
@@ -80,7 +81,7 @@ def main():
     fids = shard_frames(rank, world, total)
     epochs = sorted({f // 10 for f in fids})
     set_of = {e: i for i, e in enumerate(epochs)}
-    r = Renderer(wl.scene, Wd, H, max_frames=F, device=local)
+    r = Renderer(wl.scene, Wd, H, max_frames=F, device=local, frames_per_launch=args.frames_per_launch)
     for e in epochs:
         st = wl.epoch(e)
         r.set_instance_transforms(set_of[e], st.models)
@@ -130,18 +131,20 @@ def main():
     npx = H * Wd
     b_out = npx * (3 + 4)                                  # RGB8 + int32 instance per frame
     b_tex = int(wl.scene.texture_bytes())
-    bytes_per_launch = F * (b_out + b_tex)
-    raster_ms = tm["ms_raster"] / max(tm["batches"], 1)
+    launches = max(tm["batches"], 1)                       # k_raster launches (one per launch chain)
+    frames_per_launch = tm["frames"] / launches
+    bytes_per_launch = int(round(frames_per_launch * (b_out + b_tex)))
+    raster_ms = tm["ms_raster"] / launches
     achieved = bytes_per_launch / (raster_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.profile_json):
         try:
             pj = json.load(open(args.profile_json))
-            if pj.get("workload") == args.workload and pj.get("frames_per_step") == F:
+            if pj.get("workload") == args.workload and pj.get("frames_per_launch") == frames_per_launch:
                 traffic = pj.get("k_raster_bytes_per_launch")
         except Exception:
             traffic = None
-    stage_ms = {k: tm[k] / max(tm["batches"], 1) for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")}
+    stage_ms = {k: tm[k] / K for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")}
     b_geom = wl.scene.authored_bytes()
 
     # ---- CPU baseline (rank 0, N=1 only): the oracle on a bounded sample ----
@@ -174,7 +177,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.workload}: world2.usd + crane/dumper/4 rigged-human proxies, "
                                    f"{Wd}x{H}, RGB8 + int32 instance mask + {Kp} 2D keypoints/frame",
-                       "frames_per_step": F, "seed": args.seed, "width": Wd, "height": H,
+                       "frames_per_step": F, "frames_per_launch": frames_per_launch, "seed": args.seed, "width": Wd, "height": H,
                        "tris_per_frame": wl.scene.n_tris_per_frame,
                        "parallelism": f"seed-sharded epochs x{world}, no collectives"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -185,7 +188,8 @@ def main():
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "frame_roofline": {"B_frame": b_geom + b_tex + npx * 7,
                                "frac": round(value / world * (b_geom + b_tex + npx * 7) / (HBM_PEAK_GBS * 1e9), 5)},
-            "records_per_frame": round(bst["records"] / F, 1), "bin_entries_per_frame": round(bst["bin_entries"] / F, 1),
+            "records_per_frame": round(bst["records"] / max(bst["frames"], 1), 1),
+            "bin_entries_per_frame": round(bst["bin_entries"] / max(bst["frames"], 1), 1),
         }
         print(json.dumps(line), flush=True)
     r.close()

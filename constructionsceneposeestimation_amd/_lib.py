@@ -10,8 +10,9 @@ import os
 from typing import Optional
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 4  # CSG_ABI_VERSION in include/csg_api.h
+# CSG_LIB names an alternative build of the same ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("CSG_LIB") or os.path.join(PKG, "libcsg.so")
+ABI_VERSION = 5  # CSG_ABI_VERSION in include/csg_api.h
 KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
 
 EXPORTED = (
@@ -30,7 +31,8 @@ class CsgError(RuntimeError):
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("width", C.c_uint32), ("height", C.c_uint32),
                 ("max_frames", C.c_uint32), ("near_clip", C.c_float), ("far_clip", C.c_float),
-                ("records_per_frame", C.c_uint32), ("bins_per_frame", C.c_uint32)]
+                ("records_per_frame", C.c_uint32), ("bins_per_frame", C.c_uint32),
+                ("frames_per_launch", C.c_uint32)]
 
 
 class Mesh(C.Structure):
@@ -67,7 +69,8 @@ class Outputs(C.Structure):
 
 
 class BatchStats(C.Structure):
-    _fields_ = [("records", C.c_uint64), ("bin_entries", C.c_uint64), ("ms_setup", C.c_float),
+    _fields_ = [("records", C.c_uint64), ("bin_entries", C.c_uint64), ("frames", C.c_uint32),
+                ("pad", C.c_uint32), ("ms_setup", C.c_float),
                 ("ms_bin", C.c_float), ("ms_raster", C.c_float), ("ms_keypoints", C.c_float),
                 ("ms_total", C.c_float)]
 
@@ -85,7 +88,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(path) or os.environ.get("CSG_AUTOBUILD", "1") == "1":
+    if path == os.path.join(PKG, "libcsg.so") and (not os.path.exists(path) or
+                                                   os.environ.get("CSG_AUTOBUILD", "1") == "1"):
         try:
             from .build import build, needs_build
             if needs_build():

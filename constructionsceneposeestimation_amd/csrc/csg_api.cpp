@@ -45,6 +45,13 @@ struct DevBuf {
   }
 };
 
+// Default frames per launch chain: the whole batch.  Measured on C3 (1080p,
+// 60 frames): chains of 2/4/8/20 frames cost 3.7x/2.0x/1.6x/1.3x the time of
+// one chain -- per-launch tails and k_setup's early-exit blocks dominate, and
+// keeping records in the Infinity Cache does not pay that back.  Smaller
+// chains only bound the work-buffer memory.
+constexpr uint32_t kAutoChainFrames = 0xFFFFFFFFu;
+
 struct HostTexture {
   std::vector<uint8_t> rgba;
   uint32_t w = 0, h = 0;
@@ -122,6 +129,7 @@ struct csg_ctx {
   uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
   uint32_t bin_blocks = 128;            // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only)
   int raster_variant = 0;               // k_raster expansion variant (CSG_VARIANT overrides; A/B only)
+  uint32_t chain_frames = 0;            // frames per launch chain (cfg.frames_per_launch; CSG_CHAIN overrides)
 
   int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -159,6 +167,9 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
   if (const char* v = getenv("CSG_VARIANT")) c->raster_variant = atoi(v);
   if (const char* v = getenv("CSG_BINBLOCKS")) c->bin_blocks = std::max(1, std::min(1024, atoi(v)));
+  c->chain_frames = cfg->frames_per_launch ? cfg->frames_per_launch : kAutoChainFrames;
+  if (const char* v = getenv("CSG_CHAIN")) c->chain_frames = (uint32_t)std::max(1, atoi(v));
+  c->chain_frames = std::min(c->chain_frames, cfg->max_frames);
   c->tiles_x = (cfg->width + kTile - 1) / kTile;
   c->tiles_y = (cfg->height + kTile - 1) / kTile;
   c->n_tiles = c->tiles_x * c->tiles_y;
@@ -469,8 +480,8 @@ static int sync_scene_state(csg_ctx* c) {
   return CSG_OK;
 }
 
-static int ensure_work(csg_ctx* c, uint32_t F) {
-  const uint32_t maxF = c->cfg.max_frames;
+static int ensure_work(csg_ctx* c) {
+  const uint32_t maxF = c->chain_frames;   // work buffers hold one launch chain
   if (c->work_frames == maxF && c->rec_cap) return CSG_OK;
   if (!c->rec_cap) {
     c->rec_cap = c->cfg.records_per_frame ? c->cfg.records_per_frame
@@ -481,8 +492,9 @@ static int ensure_work(csg_ctx* c, uint32_t F) {
                                                                       0x7FFFFFFFull);
   }
   const size_t npx = (size_t)c->cfg.width * c->cfg.height;
-  HIP_TRY(c, c->frames.alloc(maxF));
-  if (!c->h_frames) HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_frames), sizeof(FrameDev) * maxF));
+  HIP_TRY(c, c->frames.alloc(c->cfg.max_frames));   // the whole batch's frame records
+  if (!c->h_frames)
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_frames), sizeof(FrameDev) * c->cfg.max_frames));
   HIP_TRY(c, c->clip.alloc((size_t)maxF * c->n_inst * 12));
   HIP_TRY(c, c->pv.alloc((size_t)maxF * 12));
   HIP_TRY(c, c->cam.alloc((size_t)maxF * kCamFloats));
@@ -518,7 +530,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     return c->fail(CSG_ERR_INVALID, "render: need 1..%u frames", c->cfg.max_frames);
   int rc = sync_scene_state(c);
   if (rc) return rc;
-  rc = ensure_work(c, F);
+  rc = ensure_work(c);
   if (rc) return rc;
   const size_t npx = (size_t)c->cfg.width * c->cfg.height;
   const bool dev = out->on_device != 0;
@@ -587,9 +599,9 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   if (!out->inst_stats) b.stats = nullptr;
   b.tile_words = (c->n_tiles + 31u) / 32u;
   if (want_kp) {
-    HIP_TRY(c, c->kp_w.alloc((size_t)F * c->n_kp));
-    HIP_TRY(c, c->kp_pix.alloc((size_t)F * c->n_kp));
-    HIP_TRY(c, c->kp_tiles.alloc((size_t)F * b.tile_words));
+    HIP_TRY(c, c->kp_w.alloc((size_t)c->chain_frames * c->n_kp));
+    HIP_TRY(c, c->kp_pix.alloc((size_t)c->chain_frames * c->n_kp));
+    HIP_TRY(c, c->kp_tiles.alloc((size_t)c->chain_frames * b.tile_words));
     b.kp_w = c->kp_w.p;
     b.kp_pix = c->kp_pix.p;
     b.kp_tiles = c->kp_tiles.p;
@@ -597,32 +609,50 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (!b.kp_vis) { HIP_TRY(c, c->o_kp_vis.alloc((size_t)F * c->n_kp)); b.kp_vis = c->o_kp_vis.p; }
   }
   SceneDev s = scene_dev(c);
-  HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * F * kCounterStride, st));
-  HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
-  HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * F * c->n_tiles, st));
-  HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), st));
-  if (want_kp) HIP_TRY(c, hipMemsetAsync(b.kp_tiles, 0, sizeof(uint32_t) * F * b.tile_words, st));
-  launch_init_stats(b, F, st);
-  if (c->timing) {
-    const uint32_t slot = (uint32_t)(c->ring_count % csg_ctx::kRing);
-    c->ev = &c->ring[(size_t)slot * 5];
-    c->ring_frames[slot] = F;
-    ++c->ring_count;
+  // The batch runs as consecutive launch chains of `chain_frames` frames (by
+  // default one chain); the work buffers hold one chain.
+  const uint32_t G = c->chain_frames;
+  for (uint32_t c0 = 0; c0 < F; c0 += G) {
+    const uint32_t Fc = std::min(G, F - c0);
+    BatchDev bc = b;
+    bc.frames = dframes + c0;
+    if (bc.rgb) bc.rgb += (size_t)c0 * npx * 3;
+    if (bc.inst) bc.inst += (size_t)c0 * npx;
+    if (bc.depth) bc.depth += (size_t)c0 * npx;
+    if (bc.normals) bc.normals += (size_t)c0 * npx * 3;
+    if (bc.points) bc.points += (size_t)c0 * npx * 3;
+    if (bc.stats) bc.stats += (size_t)c0 * b.n_labels * 5;
+    if (want_kp) {
+      bc.kp_uv += (size_t)c0 * c->n_kp * 2;
+      bc.kp_vis += (size_t)c0 * c->n_kp;
+    }
+    HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * Fc * kCounterStride, st));
+    HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
+    HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
+    if (c0 == 0) HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), st));
+    if (want_kp) HIP_TRY(c, hipMemsetAsync(bc.kp_tiles, 0, sizeof(uint32_t) * Fc * bc.tile_words, st));
+    launch_init_stats(bc, Fc, st);
+    if (c->timing) {
+      const uint32_t slot = (uint32_t)(c->ring_count % csg_ctx::kRing);
+      c->ev = &c->ring[(size_t)slot * 5];
+      c->ring_frames[slot] = Fc;
+      ++c->ring_count;
+    }
+    if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[0], st));
+    launch_clip(s, bc, Fc, st);
+    launch_setup(s, bc, c->chunks.p, c->n_chunks, Fc, st);
+    if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
+    launch_count(s, bc, Fc, c->bin_blocks, st);
+    launch_scan(s, bc, Fc, st);
+    launch_bin(s, bc, Fc, c->bin_blocks, st);
+    if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
+    launch_keypoints(s, bc, Fc, st);   // projection; k_raster depth-tests against its z-buffer
+    if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
+    launch_raster(s, bc, Fc, st, c->raster_variant);
+    if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
+    c->last_F = Fc;
   }
-  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[0], st));
-  launch_clip(s, b, F, st);
-  launch_setup(s, b, c->chunks.p, c->n_chunks, F, st);
-  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
-  launch_count(s, b, F, c->bin_blocks, st);
-  launch_scan(s, b, F, st);
-  launch_bin(s, b, F, c->bin_blocks, st);
-  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
-  launch_keypoints(s, b, F, st);   // projection; k_raster depth-tests against its z-buffer
-  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
-  launch_raster(s, b, F, st, c->raster_variant);
-  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
   HIP_TRY(c, hipGetLastError());
-  c->last_F = F;
   if (!dev) {
     if (out->rgb) HIP_TRY(c, hipMemcpyAsync(out->rgb, b.rgb, F * npx * 3, hipMemcpyDeviceToHost, st));
     if (out->instance) HIP_TRY(c, hipMemcpyAsync(out->instance, b.inst, F * npx * 4, hipMemcpyDeviceToHost, st));
@@ -685,6 +715,7 @@ int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
   memset(st, 0, sizeof(*st));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   const uint32_t F = c->last_F;
+  st->frames = F;
   if (!F) return CSG_OK;
   std::vector<uint32_t> rcs((size_t)F * kCounterStride), rc(F), to((size_t)F * (c->n_tiles + 1));
   HIP_TRY(c, hipMemcpy(rcs.data(), c->rec_count.p, rcs.size() * 4, hipMemcpyDeviceToHost));

@@ -634,8 +634,8 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
 // tile origin) do the exact arithmetic in 32 bits with full-rate 24-bit
 // multiplies; others in int64.
 template <bool Small>
-__device__ __forceinline__ void row_span(const Rec& R, int ox, int oy, int ly, int x0, int x1, int& xl, int& xr,
-                                         bool no_exact) {
+__device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, int ox, int oy, int ly, int x0, int x1,
+                                         int& xl, int& xr, bool no_exact) {
   using T = typename std::conditional<Small, int32_t, int64_t>::type;
   const int32_t OX = ox * 256, OY = oy * 256;
   const int32_t cy = ly * 256 + 128;
@@ -645,8 +645,8 @@ __device__ __forceinline__ void row_span(const Rec& R, int ox, int oy, int ly, i
   const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
-    const int32_t ax = R.x[ea[e]] - OX, ay = R.y[ea[e]] - OY;
-    const int32_t dx = R.x[eb[e]] - R.x[ea[e]], dy = R.y[eb[e]] - R.y[ea[e]];
+    const int32_t ax = RX[ea[e]] - OX, ay = RY[ea[e]] - OY;
+    const int32_t dx = RX[eb[e]] - RX[ea[e]], dy = RY[eb[e]] - RY[ea[e]];
     const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
     if constexpr (Small) c0[e] = __mul24(dx, cy - ay) + __mul24(dy, ax) + bias;
     else c0[e] = (int64_t)dx * (cy - ay) + (int64_t)dy * ax + bias;
@@ -692,38 +692,56 @@ struct RasterCtx {
   uint32_t dbg;
 };
 
-// One fragment of record R at tile pixel (lx, ly), already known to be
+// LDS image of up to 256 staged records as seven 16-B field groups (the Rec
+// layout cut at 16-B boundaries), group-major: lanes reading one group of
+// different records hit consecutive 16-B slots (no bank conflicts; a Rec-
+// strided image puts 8 records on each set of banks), lanes reading the same
+// record broadcast.  Groups: 0 x0 x1 x2 y0 | 1 y1 y2 p0 p1 | 2 uid atex A0 A1 |
+// 3 A2 B0 B1 B2 | 4 C0 C1 C2 invdet | 5 uv0-3 | 6 uv4 uv5 atex_wh athr.
+constexpr int kRecGroups = (int)(sizeof(Rec) / 16);
+struct RecImage {
+  uint4 q[kRecGroups][kBlock];
+};
+
+__device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
+
+// One fragment of staged record k at tile pixel (lx, ly), already known to be
 // covered: homogeneous depth, depth range, early-z against the LDS key,
 // alpha test (texture described inline in the record), then ds_min_u64.
-__device__ __forceinline__ void fragment(const RasterCtx& c, const Rec& R, int lx, int ly) {
+__device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, int k, int lx, int ly) {
   const int px = c.ox + lx, py = c.oy + ly;
+  const uint4 g2 = I.q[2][k], g3 = I.q[3][k], g4 = I.q[4][k];
+  const float A[3] = {f_(g2.z), f_(g2.w), f_(g3.x)}, B[3] = {f_(g3.y), f_(g3.z), f_(g3.w)};
+  const float C[3] = {f_(g4.x), f_(g4.y), f_(g4.z)};
   float e[3], ssum, invw;
-  hom_eval(R.A, R.B, R.C, R.invdet, px, py, e, ssum, invw);
+  hom_eval(A, B, C, f_(g4.w), px, py, e, ssum, invw);
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
-  const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | R.uid;
+  const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
   if (!(c.dbg & 16u) && key >= *z) return;
-  if (!(c.dbg & 4u) && R.atex != kNoAlpha) {
+  if (!(c.dbg & 4u) && g2.y != kNoAlpha) {
+    const uint4 g5 = I.q[5][k], g6 = I.q[6][k];
+    const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
     float u, v;
-    interp_uv(e, ssum, R.uv, u, v);
-    if (!(tex_alpha(c.aquad, R.atex, R.atex_wh, u, v) > (int)R.athr)) return;
+    interp_uv(e, ssum, uv, u, v);
+    if (!(tex_alpha(c.aquad, g2.y, g6.z, u, v) > (int)g6.w)) return;
   }
   atomicMin(z, key);
 }
 
 // Stage bin entry `idx` into `slot`; returns its row count inside the tile.
 __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t* bins, uint32_t idx, uint32_t end,
-                                                 uint32_t rec_cap, Rec* slot, int ox, int oy, uint32_t& row0) {
+                                                 uint32_t rec_cap, RecImage& img, int slot, int ox, int oy,
+                                                 uint32_t& row0) {
   row0 = 0;
   const uint32_t r = (idx < end) ? bins[idx] : 0xFFFFFFFFu;
   if (r >= rec_cap) return 0;
   const uint4* src = reinterpret_cast<const uint4*>(recs + r);
-  uint4* dst = reinterpret_cast<uint4*>(slot);
-  uint4 q[7];
+  uint4 q[kRecGroups];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) q[k] = src[k];
+  for (int k = 0; k < kRecGroups; ++k) q[k] = src[k];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) dst[k] = q[k];
+  for (int k = 0; k < kRecGroups; ++k) img.q[k][slot] = q[k];
   const uint32_t p0 = q[1].z, p1 = q[1].w;            // px0 | py0 << 16, px1 | py1 << 16
   int y0 = max((int)(p0 >> 16), oy), y1 = min((int)(p1 >> 16), oy + kTile - 1);
   const int x0 = max((int)(p0 & 0xFFFFu), ox), x1 = min((int)(p1 & 0xFFFFu), ox + kTile - 1);
@@ -769,7 +787,7 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 
 template <int V>
 struct RasterLds {
-  Rec lrec[kBlock];                     // 28 KiB staged bin records
+  RecImage img;                         // 28 KiB staged bin records
   uint32_t pre[kBlock + 1];             // row-item prefix per record
   uint8_t row0[kBlock];                 // first tile row of each staged record | 0x80 if small
   uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
@@ -789,7 +807,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
   const int tid = threadIdx.x;
   for (uint32_t base = beg; base < end; base += kBlock) {
     uint32_t row0;
-    const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, &L.lrec[tid], c.ox, c.oy, row0);
+    const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
     L.row0[tid] = (uint8_t)row0;
     if ((b.dbg & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
       atomicAdd(&b.overflow[1], 1u);
@@ -806,14 +824,16 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
       int xl = 0;
       if (j1 < tot1) {
         const int k = find_item(L.pre, j1);
-        const Rec& R = L.lrec[k];
-        const int x0 = max((int)R.px0 - c.ox, 0), x1 = min((int)R.px1 - c.ox, kTile - 1);
+        const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
+        const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
+        const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
+        const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTile - 1);
         const uint32_t r0b = L.row0[k];
         const int ly = (int)(r0b & 31u) + (int)(j1 - L.pre[k]);
         int xr;
         if (b.dbg & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
-        else if (r0b & 0x80u) row_span<true>(R, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
-        else row_span<false>(R, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
+        else if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
+        else row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
         if (xl <= xr) {
           w2 = (uint32_t)(xr - xl + 1);
           sp = (uint32_t)k | ((uint32_t)ly << 8);
@@ -838,7 +858,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         if constexpr (V == 1) s2 = L.owner[j];
         else s2 = find_item(L.pre2, j);
         const uint32_t spj = L.span[s2];
-        fragment(c, L.lrec[spj & 255u], (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
+        fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
     }

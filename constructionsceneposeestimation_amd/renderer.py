@@ -49,14 +49,15 @@ def _light_struct(light) -> "_lib.Light":
 
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, max_frames: int = 8, device: int = 0,
-                 intrinsics: Optional[Intrinsics] = None, records_per_frame: int = 0, bins_per_frame: int = 0):
+                 intrinsics: Optional[Intrinsics] = None, records_per_frame: int = 0, bins_per_frame: int = 0,
+                 frames_per_launch: int = 0):
         self.lib = _lib.load()
         self.scene = scene
         self.width, self.height = int(width), int(height)
         self.max_frames = int(max_frames)
         self.intr = intrinsics or Intrinsics(self.width, self.height)
         cfg = _lib.Config(device, self.width, self.height, self.max_frames, self.intr.near, self.intr.far,
-                          records_per_frame, bins_per_frame)
+                          records_per_frame, bins_per_frame, frames_per_launch)
         ctx = C.c_void_p()
         rc = self.lib.csg_create(C.byref(cfg), C.byref(ctx))
         if rc != 0:

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 4
+#define CSG_ABI_VERSION 5
 
 typedef enum {
   CSG_OK = 0,
@@ -60,6 +60,9 @@ typedef struct {
   float near_clip, far_clip; /* 0.5 / 250 m, generate_construction_data.py:1437 */
   uint32_t records_per_frame;/* raster-triangle capacity per frame (0 = auto) */
   uint32_t bins_per_frame;   /* tile-bin entry capacity per frame (0 = auto) */
+  uint32_t frames_per_launch;/* frames per kernel chain inside a batch (0 = the whole batch):
+                                work buffers are sized for one chain, so this bounds their
+                                memory independently of max_frames */
 } csg_config;
 
 typedef struct {
@@ -118,8 +121,10 @@ typedef struct {
 } csg_outputs;
 
 typedef struct {
-  uint64_t records;          /* raster triangles emitted (all frames of the last batch) */
-  uint64_t bin_entries;      /* tile-bin entries */
+  uint64_t records;          /* raster triangles emitted (all frames of the last launch chain) */
+  uint64_t bin_entries;      /* tile-bin entries (same frames) */
+  uint32_t frames;           /* frames of the last launch chain */
+  uint32_t pad;
   float ms_setup, ms_bin, ms_raster, ms_keypoints, ms_total;   /* HIP-event timings */
 } csg_batch_stats;
 
@@ -158,12 +163,12 @@ int csg_synchronize(csg_ctx* ctx);
 int csg_get_batch_stats(csg_ctx* ctx, csg_batch_stats* st);
 
 /* Per-stage device time accumulated with HIP events recorded on the launch
- * stream for every batch since the last reset (no host sync inside the
- * timed loop).  Stages: setup = k_clip+k_setup, bin = k_count+k_scan+k_bin,
+ * stream for every launch chain since the last reset (no host sync inside
+ * the timed loop); `batches` counts launch chains.  Stages: setup = k_clip+k_setup, bin = k_count+k_scan+k_bin,
  * keypoints = k_keypoints (projection), raster = k_raster (tile raster,
  * keypoint depth test, resolve). */
 typedef struct {
-  uint32_t batches;          /* batches accumulated (capped at the ring size, 4096) */
+  uint32_t batches;          /* launch chains accumulated (capped at the ring size, 4096) */
   uint32_t frames;           /* frames in those batches */
   double ms_setup, ms_bin, ms_raster, ms_keypoints;
 } csg_timing;

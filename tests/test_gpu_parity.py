@@ -75,6 +75,26 @@ def test_batch_vs_single(world2):
             assert np.array_equal(batch[key][k], singles[k][key][0])
 
 
+def test_launch_chains(world2):
+    """A batch split into launch chains (frames_per_launch) gives the same
+    bytes as one chain, for every output including keypoints and stats."""
+    from constructionsceneposeestimation_amd.renderer import Renderer
+    W, H = 640, 360
+    views, projs = pose_frames(WORLD2_POSES[:5], W, H)
+    fr = _frames(views, projs)
+    kp = np.random.default_rng(3).uniform(-12, 12, (64, 3)).astype(np.float32)
+    kp[:, 2] = np.abs(kp[:, 2]) * 0.3
+    want = ("rgb", "instance", "depth", "keypoints", "stats", "normals", "points")
+    outs = []
+    for chain in (5, 2, 1):
+        with Renderer(world2, W, H, max_frames=5, frames_per_launch=chain) as r:
+            r.set_keypoints(0, kp)
+            outs.append(r.render(fr, want=want))
+    for o in outs[1:]:
+        for key, a in outs[0].items():
+            assert np.array_equal(a.view(np.uint8), o[key].view(np.uint8)), key
+
+
 def _assert_extra(gpu, ora, f):
     gn, on = gpu["normals"][f].view(np.uint16), ora["normals"].view(np.uint16)
     assert np.array_equal(gn, on), f"frame {f}: normals differ at {np.argwhere((gn != on).any(-1))[:5].tolist()}"
