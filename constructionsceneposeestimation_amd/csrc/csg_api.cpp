@@ -128,7 +128,6 @@ struct csg_ctx {
   uint32_t last_F = 0;
   uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
   uint32_t bin_blocks = 128;            // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only)
-  int raster_variant = 0;               // k_raster expansion variant (CSG_VARIANT overrides; A/B only)
   uint32_t chain_frames = 0;            // frames per launch chain (cfg.frames_per_launch; CSG_CHAIN overrides)
 
   int fail(int code, const char* fmt, ...) {
@@ -165,7 +164,6 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   csg_ctx* c = new csg_ctx();
   c->cfg = *cfg;
   if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
-  if (const char* v = getenv("CSG_VARIANT")) c->raster_variant = atoi(v);
   if (const char* v = getenv("CSG_BINBLOCKS")) c->bin_blocks = std::max(1, std::min(1024, atoi(v)));
   c->chain_frames = cfg->frames_per_launch ? cfg->frames_per_launch : kAutoChainFrames;
   if (const char* v = getenv("CSG_CHAIN")) c->chain_frames = (uint32_t)std::max(1, atoi(v));
@@ -648,7 +646,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
     launch_keypoints(s, bc, Fc, st);   // projection; k_raster depth-tests against its z-buffer
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
-    launch_raster(s, bc, Fc, st, c->raster_variant);
+    launch_raster(s, bc, Fc, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
     c->last_F = Fc;
   }

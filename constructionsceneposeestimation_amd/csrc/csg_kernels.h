@@ -47,6 +47,7 @@ struct __attribute__((aligned(16))) Rec {
   uint32_t athr;               // 4 : alpha threshold (keep iff alpha > athr)
 };
 static_assert(sizeof(Rec) == 112, "Rec layout");
+constexpr int kRecGroups = 7;  // 16-B field groups k_raster stages (the 112 B of payload)
 
 struct FrameDev {                // csg_frame mirror
   float view[16];
@@ -118,7 +119,7 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
-void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st, int variant);
+void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_inst_bounds(const SceneDev& s, const Chunk* chunks, uint32_t n_chunks, const float* models,

@@ -318,7 +318,7 @@ __device__ __forceinline__ void store_rec(Rec* dst, const Rec& r) {
   const uint4* src = reinterpret_cast<const uint4*>(&r);
   uint4* d = reinterpret_cast<uint4*>(dst);
 #pragma unroll
-  for (int k = 0; k < 7; ++k) d[k] = src[k];
+  for (int k = 0; k < kRecGroups; ++k) d[k] = src[k];
 }
 
 __device__ __forceinline__ uint32_t rect_area(uint32_t rc) {
@@ -692,15 +692,32 @@ struct RasterCtx {
   uint32_t dbg;
 };
 
-// LDS image of up to 256 staged records as seven 16-B field groups (the Rec
+// LDS image of up to kStage staged records as seven 16-B field groups (the Rec
 // layout cut at 16-B boundaries), group-major: lanes reading one group of
 // different records hit consecutive 16-B slots (no bank conflicts; a Rec-
 // strided image puts 8 records on each set of banks), lanes reading the same
 // record broadcast.  Groups: 0 x0 x1 x2 y0 | 1 y1 y2 p0 p1 | 2 uid atex A0 A1 |
 // 3 A2 B0 B1 B2 | 4 C0 C1 C2 invdet | 5 uv0-3 | 6 uv4 uv5 atex_wh athr.
-constexpr int kRecGroups = (int)(sizeof(Rec) / 16);
+//
+// Occupancy: k_raster is latency-bound (LDS and VMEM dependency chains), and
+// waves per SIMD are its lever (measured on C3: 3 waves +22% time vs 4, 5 waves
+// -8% vs 4).  Five 256-thread workgroups per CU need <= 32 KiB of LDS each
+// (176 staged records, 192 shade-table slots) and <= 96 VGPRs.
+#ifndef CSG_STAGE
+#define CSG_STAGE 176
+#endif
+#ifndef CSG_WAVES
+#define CSG_WAVES 5             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
+#endif
+#if CSG_WAVES > 0
+#define CSG_RASTER_ATTR __attribute__((amdgpu_waves_per_eu(CSG_WAVES, CSG_WAVES)))
+#else
+#define CSG_RASTER_ATTR
+#endif
+constexpr int kStage = CSG_STAGE;     // records staged per raster batch (<= kBlock)
+static_assert(kStage <= kBlock, "one staged record per thread");
 struct RecImage {
-  uint4 q[kRecGroups][kBlock];
+  uint4 q[kRecGroups][kStage];
 };
 
 __device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
@@ -734,7 +751,7 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
                                                  uint32_t rec_cap, RecImage& img, int slot, int ox, int oy,
                                                  uint32_t& row0) {
   row0 = 0;
-  const uint32_t r = (idx < end) ? bins[idx] : 0xFFFFFFFFu;
+  const uint32_t r = (idx < end && slot < kStage) ? bins[idx] : 0xFFFFFFFFu;
   if (r >= rec_cap) return 0;
   const uint4* src = reinterpret_cast<const uint4*>(recs + r);
   uint4 q[kRecGroups];
@@ -785,7 +802,6 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
   return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
 
-template <int V>
 struct RasterLds {
   RecImage img;                         // 28 KiB staged bin records
   uint32_t pre[kBlock + 1];             // row-item prefix per record
@@ -793,19 +809,17 @@ struct RasterLds {
   uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
   uint32_t pre2[kBlock + 1];            // pixel-item prefix per span
   uint32_t wsum[kBlock / 64];
-  uint8_t owner[V == 1 ? kBlock * kTile : 4];   // V1: span of every pixel item
 };
-static_assert(sizeof(RasterLds<0>) + kTilePix * 8 <= 40960, "k_raster<0> LDS must allow 4 workgroups per CU");
 
-// Block-level two-level expansion of 256-record batches.
+// Block-level two-level expansion of kStage-record batches.
 //   level 1: (record, row) items, one per thread -> exact row span
-//   level 2: (span, pixel) items; V0 finds each item's span by binary search
-//            over the span prefix, V1 reads it from a per-item owner map.
-template <int V>
-__device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds<V>& L, uint32_t beg,
+//   level 2: (span, pixel) items; each finds its span by a 4-ary search over
+//            the span prefix (a per-item owner map measured slower: its LDS
+//            cost a workgroup per CU).
+__device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds& L, uint32_t beg,
                                              uint32_t end, const uint32_t* bins, const Rec* recs) {
   const int tid = threadIdx.x;
-  for (uint32_t base = beg; base < end; base += kBlock) {
+  for (uint32_t base = beg; base < end; base += kStage) {
     uint32_t row0;
     const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
     L.row0[tid] = (uint8_t)row0;
@@ -846,18 +860,11 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
       uint32_t tot2;
       const uint32_t ex2 = block_excl_scan(w2, L.wsum, tot2);
       L.span[tid] = sp | ((ex2 - (uint32_t)xl + 32u) << 16);
-      if constexpr (V == 1) {
-        for (uint32_t q = 0; q < w2; ++q) L.owner[ex2 + q] = (uint8_t)tid;
-      } else {
-        L.pre2[tid] = ex2;
-        if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
-      }
+      L.pre2[tid] = ex2;
+      if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
       __syncthreads();
       for (uint32_t j = tid; j < ((b.dbg & 8u) ? 0u : tot2); j += kBlock) {
-        int s2;
-        if constexpr (V == 1) s2 = L.owner[j];
-        else s2 = find_item(L.pre2, j);
-        const uint32_t spj = L.span[s2];
+        const uint32_t spj = L.span[find_item(L.pre2, j)];
         fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
@@ -882,66 +889,75 @@ struct ShadeEntry {
 // Triangle setup of the resolve, exactly as csg_oracle.c: clip coordinates,
 // homogeneous coefficients, material, uvs, flat two-sided Lambert from the
 // world-space face normal.
+// `e` is the triangle's LDS slot: fields are stored as soon as they are
+// known, and the clip and model rows are consumed one at a time, so few
+// values are live at once (this phase sets the kernel's register budget).
 __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b, uint32_t f, uint32_t uid,
                                             ShadeEntry& e) {
   const uint32_t i = uid >> kUidShift, t = uid & (kMaxTrisPerMesh - 1u);
-  const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
-  const float* M = b.models + ((size_t)b.frames[f].xform_set * s.n_inst + i) * 16;
+  const uint32_t set = b.frames[f].xform_set;
   const InstDesc m = s.inst[i];
-  float c[12], mm[12];
-#pragma unroll
-  for (int z = 0; z < 12; ++z) { c[z] = Cm[z]; mm[z] = M[z]; }
   const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
-  float pobj[3][3];
-  Cv3 v[3];
+  float p[9];
 #pragma unroll
-  for (int z = 0; z < 3; ++z) {
-    const float* p = tp + 3 * z;
-    pobj[z][0] = p[0]; pobj[z][1] = p[1]; pobj[z][2] = p[2];
-    v[z].x = dot4(c + 0, p[0], p[1], p[2]);
-    v[z].y = dot4(c + 4, p[0], p[1], p[2]);
-    v[z].w = dot4(c + 8, p[0], p[1], p[2]);
+  for (int z = 0; z < 9; ++z) p[z] = tp[z];
+  Cv3 v[3];
+  {
+    const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
+#pragma unroll
+    for (int z = 0; z < 3; ++z) {
+      v[z].x = dot4(Cm + 0, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
+      v[z].y = dot4(Cm + 4, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
+      v[z].w = dot4(Cm + 8, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
+    }
   }
   Hom h;
   hom_setup(v, h);
 #pragma unroll
   for (int z = 0; z < 3; ++z) { e.A[z] = h.A[z]; e.B[z] = h.B[z]; e.C[z] = h.C[z]; }
   e.invdet = h.invdet;
+  const bool facing = h.invdet < 0.0f;
   e.label = m.label;
-  const uint32_t set = b.frames[f].xform_set;
   const MatDesc mat = b.mats[(size_t)set * b.n_mat + m.material];
-  const LightDev& L = b.lights[set];
-  e.tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
+  const int tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
+  e.tex = tex;
   e.base = (uint32_t)mat.base[0] | ((uint32_t)mat.base[1] << 8) | ((uint32_t)mat.base[2] << 16);
   const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
 #pragma unroll
-  for (int z = 0; z < 6; ++z) e.uv[z] = e.tex >= 0 ? tu[z] : 0.0f;
-  float pw[3][3];
+  for (int z = 0; z < 6; ++z) e.uv[z] = tex >= 0 ? tu[z] : 0.0f;
+  // world-space edges e1 = pw1 - pw0, e2 = pw2 - pw0, one model row (= one
+  // world coordinate) at a time
+  float e1[3], e2[3];
+  {
+    const float* M = b.models + ((size_t)set * s.n_inst + i) * 16;
 #pragma unroll
-  for (int z = 0; z < 3; ++z) {
-    pw[z][0] = dot4(mm + 0, pobj[z][0], pobj[z][1], pobj[z][2]);
-    pw[z][1] = dot4(mm + 4, pobj[z][0], pobj[z][1], pobj[z][2]);
-    pw[z][2] = dot4(mm + 8, pobj[z][0], pobj[z][1], pobj[z][2]);
+    for (int r = 0; r < 3; ++r) {
+      const float w0 = dot4(M + 4 * r, p[0], p[1], p[2]);
+      const float w1 = dot4(M + 4 * r, p[3], p[4], p[5]);
+      const float w2 = dot4(M + 4 * r, p[6], p[7], p[8]);
+      e1[r] = w1 - w0;
+      e2[r] = w2 - w0;
+    }
   }
-  const float e1x = pw[1][0] - pw[0][0], e1y = pw[1][1] - pw[0][1], e1z = pw[1][2] - pw[0][2];
-  const float e2x = pw[2][0] - pw[0][0], e2y = pw[2][1] - pw[0][1], e2z = pw[2][2] - pw[0][2];
-  const float nx = e1y * e2z - e1z * e2y;
-  const float ny = e1z * e2x - e1x * e2z;
-  const float nz = e1x * e2y - e1y * e2x;
+  const float nx = e1[1] * e2[2] - e1[2] * e2[1];
+  const float ny = e1[2] * e2[0] - e1[0] * e2[2];
+  const float nz = e1[0] * e2[1] - e1[1] * e2[0];
   const float nn = (nx * nx + ny * ny) + nz * nz;
+  const LightDev& L = b.lights[set];
   float cs = 0.0f;
-  e.n01 = 0;
-  e.n2 = 0;
+  uint32_t n01 = 0, n2 = 0;
   if (nn > 0.0f) {
     const float len = sqrtf(nn);
     const float d = (nx * L.sun_dir[0] + ny * L.sun_dir[1]) + nz * L.sun_dir[2];
     cs = fabsf(d / len);
     // two-sided: the clip-space determinant is negative exactly when the face
     // normal points toward the camera (pixel projection with fx*fy > 0)
-    const float sg = h.invdet < 0.0f ? 1.0f : -1.0f;
-    e.n01 = half_bits(sg * (nx / len)) | (half_bits(sg * (ny / len)) << 16);
-    e.n2 = half_bits(sg * (nz / len));
+    const float sg = facing ? 1.0f : -1.0f;
+    n01 = half_bits(sg * (nx / len)) | (half_bits(sg * (ny / len)) << 16);
+    n2 = half_bits(sg * (nz / len));
   }
+  e.n01 = n01;
+  e.n2 = n2;
   uint32_t q[3];
 #pragma unroll
   for (int z = 0; z < 3; ++z) {
@@ -981,36 +997,49 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
 }
 
 // Resolve-phase LDS (aliases the raster loop's): the tile's distinct winning
-// triangles in a 256-slot open-addressing table, each set up once by one
-// thread, then read by every pixel that shows it.
-constexpr uint32_t kShadeSlots = kBlock;
+// triangles in an open-addressing table of kShadeSlots, each set up once by
+// one thread, then read by every pixel that shows it.
+#ifndef CSG_SHADE_SLOTS
+#define CSG_SHADE_SLOTS 192
+#endif
+constexpr uint32_t kShadeSlots = CSG_SHADE_SLOTS;   // <= kBlock (one setup thread per slot)
+static_assert(kShadeSlots <= (uint32_t)kBlock && kShadeSlots < 255u, "one setup thread per slot; 8-bit slot ids");
 constexpr int kShadeProbes = 16;
 struct ResolveLds {
   uint32_t keys[kShadeSlots];       // uid or kNoAlpha (empty)
+  uint32_t more;                    // a pixel is left for another round
   ShadeEntry tab[kShadeSlots];
   uint32_t lstat[5][kMaxLdsLabels]; // per-label pixel count + box
 };
 
+// The resolve's LDS aliases the raster loop's in a union inside k_raster.
+static_assert((sizeof(RasterLds) > sizeof(ResolveLds) ? sizeof(RasterLds) : sizeof(ResolveLds)) + kTilePix * 8 <=
+                  (CSG_WAVES >= 5 ? 32768u : 40960u),
+              "k_raster LDS must allow CSG_WAVES workgroups per CU");
+
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
 __device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
-  const uint32_t h = (uid * 2654435761u) >> 24;
+  const uint32_t h = __umulhi(uid * 2654435761u, kShadeSlots);   // [0, kShadeSlots)
 #pragma clang loop vectorize(disable) unroll(disable)
   for (int p = 0; p < kShadeProbes; ++p) {
-    const uint32_t idx = (h + (uint32_t)p) & (kShadeSlots - 1u);
+    uint32_t idx = h + (uint32_t)p;
+    idx = idx >= kShadeSlots ? idx - kShadeSlots : idx;
     const uint32_t prev = atomicCAS(&keys[idx], kNoAlpha, uid);
     if (prev == kNoAlpha || prev == uid) return (int)idx;
   }
   return -1;
 }
 
-template <int V>
-__global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
+__global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, BatchDev b) {
   __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
+#ifdef CSG_LDS_PAD
+  __shared__ volatile uint32_t ldspad[CSG_LDS_PAD / 4];   // A/B only: occupancy probe
+  if (b.dbg == 0xDEADu) ldspad[threadIdx.x] = 1u;
+#endif
   __shared__ union Lds {
-    RasterLds<V> r;                                  // raster loop
+    RasterLds r;                                     // raster loop
     ResolveLds q;                                    // resolve
   } L;
-  static_assert(sizeof(ResolveLds) <= sizeof(RasterLds<V>), "resolve LDS must fit in the raster loop's");
   const int tid = threadIdx.x;
   const uint32_t tile = blockIdx.x, f = blockIdx.y;
   const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
@@ -1022,7 +1051,7 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
   RasterCtx c{s.aquad, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg};
   __syncthreads();
-  raster_block<V>(c, b, L.r, beg, end, bins, recs);
+  raster_block(c, b, L.r, beg, end, bins, recs);
   __syncthreads();
 
   if (b.dbg & 1u) {   // ablation: keep the raster loop alive, skip the resolve
@@ -1047,76 +1076,78 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
   for (uint32_t l = tid; l < nl; l += kBlock) {
     lstat[0][l] = 0; lstat[1][l] = 0xFFFFFFFFu; lstat[2][l] = 0xFFFFFFFFu; lstat[3][l] = 0; lstat[4][l] = 0;
   }
-  L.q.keys[tid] = kNoAlpha;
-  __syncthreads();
-  // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads
+  // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads.
+  // Rounds: the tile's distinct winning triangles go into the shade table
+  // (up to kShadeSlots per round), each is set up once by one thread, then
+  // every pixel showing it is shaded from the table.  Pixels whose triangle
+  // found no slot wait for the next round (normally there is one round).
+  // A shaded pixel's z-buffer word is dead, so it takes the pixel's result
+  // (rgb | id << 32) until the vector stores at the end: between phases a
+  // thread keeps only bit masks and slot numbers in registers.
   const int ly = tid >> 3, lx0 = (tid & 7) * 4;
   const int py = oy + ly;
   const bool row_ok = py < (int)s.H;
-  unsigned long long key[4];
-  int slot[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int px = ox + lx0 + k;
-    key[k] = (row_ok && px < (int)s.W) ? zb[ly * kTile + lx0 + k] : kEmptyKey;
-    slot[k] = -1;
-    if (key[k] != kEmptyKey) {
-      if (k > 0 && key[k - 1] != kEmptyKey && (uint32_t)key[k - 1] == (uint32_t)key[k]) slot[k] = slot[k - 1];
-      else slot[k] = shade_slot(L.q.keys, (uint32_t)key[k]);
-    }
-  }
-  __syncthreads();
-  {  // one thread per occupied slot: set the triangle up once for the whole tile
-    const uint32_t u = L.q.keys[tid];
-    if (u != kNoAlpha) {
-      ShadeEntry e;
-      if (b.dbg & 8192u) {   // ablation only: no triangle setup (garbage shading)
-        e = ShadeEntry{};
-        e.invdet = 1.0f; e.tex = -1; e.label = 0;
-      } else {
-        shade_setup(s, b, f, u, e);
-      }
-      L.q.tab[tid] = e;
-    }
-  }
-  __syncthreads();
-  const size_t npx = (size_t)s.W * s.H;
-  const uint32_t sky = b.lights[b.frames[f].xform_set].sky & 0xFFFFFFu;
-  if (row_ok) {
-    uint32_t rgb[4];
-    int32_t ids[4];
-    float dep[4];
-    uint32_t nrm[4][2];
-    uint32_t last_uid = 0xFFFFFFFFu;   // overflow path (probe run full): private setup
-    ShadeEntry own;
+  const int px0 = ox + lx0;
+  unsigned long long* zrow = &zb[ly * kTile + lx0];
+  uint32_t pend = 0;                 // bit k: pixel k still to shade
+  {
+    const uint32_t sky = b.lights[b.frames[f].xform_set].sky & 0xFFFFFFu;
+    const unsigned long long bgword = (unsigned long long)sky | (0xFFFFFFFFull << 32);   // id -1
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int px = ox + lx0 + k;
-      nrm[k][0] = nrm[k][1] = 0;
-      if (key[k] == kEmptyKey) {
-        rgb[k] = sky;
-        ids[k] = -1;
-        dep[k] = INFINITY;
-      } else if (slot[k] >= 0) {
-        const ShadeEntry& e = L.q.tab[slot[k]];
-        shade_pixel(s, e, px, py, rgb[k], ids[k], dep[k]);
-        if (b.normals) { nrm[k][0] = e.n01; nrm[k][1] = e.n2; }
-      } else {
-        if ((uint32_t)key[k] != last_uid) {
-          last_uid = (uint32_t)key[k];
-          shade_setup(s, b, f, last_uid, own);
+      const bool in = row_ok && px0 + k < (int)s.W;
+      if (in && zrow[k] != kEmptyKey) pend |= 1u << k;
+      else zrow[k] = bgword;         // background (or outside the frame)
+    }
+  }
+  const size_t npx = (size_t)s.W * s.H;
+  const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
+  const uint32_t bgmask = row_ok ? (~pend & 15u) : 0u;   // background pixels inside the frame
+  for (bool first = true;; first = false) {
+    if ((uint32_t)tid < kShadeSlots) L.q.keys[tid] = kNoAlpha;
+    __syncthreads();
+    // every thread has read the previous round's flag (it reached this
+    // barrier) and none sets it before the next barrier
+    if (tid == 0) L.q.more = 0;
+    uint32_t slots = 0xFFFFFFFFu;    // 8 bits per pixel (0xFF: none this round)
+    {
+      uint32_t prev_uid = 0xFFFFFFFFu, prev_slot = 0xFFu;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((pend >> k) & 1u) {
+          const uint32_t uid = (uint32_t)zrow[k];
+          uint32_t sl;
+          if (uid == prev_uid) sl = prev_slot;
+          else {
+            const int r = shade_slot(L.q.keys, uid);
+            sl = r < 0 ? 0xFFu : (uint32_t)r;
+          }
+          prev_uid = uid;
+          prev_slot = sl;
+          slots = (slots & ~(0xFFu << (8 * k))) | (sl << (8 * k));
+        } else {
+          prev_uid = 0xFFFFFFFFu;
         }
-        shade_pixel(s, own, px, py, rgb[k], ids[k], dep[k]);
-        if (b.normals) { nrm[k][0] = own.n01; nrm[k][1] = own.n2; }
       }
     }
-    // label stats, one set of LDS atomics per run of equal labels
-    int32_t run = -1;
-    uint32_t cnt = 0, xmin = 0, xmax = 0;
-#pragma unroll
-    for (int k = 0; k <= 4; ++k) {
-      const int32_t lab = k < 4 ? ids[k] : -2;
-      if (lab != run) {
+    __syncthreads();
+    {  // one thread per occupied slot: set the triangle up once for the whole tile
+      const uint32_t u = (uint32_t)tid < kShadeSlots ? L.q.keys[tid] : kNoAlpha;
+      if (u != kNoAlpha) {
+        ShadeEntry& e = L.q.tab[tid];
+        if (b.dbg & 8192u) {   // ablation only: no triangle setup (garbage shading)
+          e = ShadeEntry{};
+          e.invdet = 1.0f; e.tex = -1; e.label = 0;
+        } else {
+          shade_setup(s, b, f, u, e);
+        }
+      }
+    }
+    __syncthreads();
+    if (row_ok) {
+      int32_t run = -1;              // label stats, one set of LDS atomics per run of equal labels
+      uint32_t cnt = 0, xmin = 0, xmax = 0;
+      auto flush_run = [&]() {
         if (run >= 0 && (uint32_t)run < nl) {
           atomicAdd(&lstat[0][run], cnt);
           atomicMin(&lstat[1][run], xmin);
@@ -1124,39 +1155,69 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
           atomicMax(&lstat[3][run], xmax);
           atomicMax(&lstat[4][run], (uint32_t)py);
         }
-        run = lab;
-        cnt = 0;
-        xmin = (uint32_t)(ox + lx0 + k);
-      }
-      ++cnt;
-      xmax = (uint32_t)(ox + lx0 + k);
-    }
-    const int px0 = ox + lx0;
-    const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
-    float pts[4][3];
-    if (b.points) {
-      const float* cam = b.cam + (size_t)f * kCamFloats;
+      };
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (key[k] == kEmptyKey) pts[k][0] = pts[k][1] = pts[k][2] = __builtin_nanf("");
-        else unproject(cam, px0 + k, py, dep[k], pts[k]);
+        const int px = px0 + k;
+        const uint32_t sl = (slots >> (8 * k)) & 0xFFu;
+        // background pixels are written in the first round; the optional
+        // outputs are stored per pixel so their values are never live long
+        const bool bg = first && ((bgmask >> k) & 1u);
+        if (sl == 0xFFu && !bg) continue;
+        float dep = INFINITY;
+        uint32_t n01 = 0, n2 = 0;
+        if (!bg) {
+          const ShadeEntry& e = L.q.tab[sl];
+          uint32_t rgb;
+          int32_t id;
+          shade_pixel(s, e, px, py, rgb, id, dep);
+          n01 = e.n01;
+          n2 = e.n2;
+          zrow[k] = (unsigned long long)rgb | ((unsigned long long)(uint32_t)id << 32);
+          pend &= ~(1u << k);
+          if (id != run) {
+            flush_run();
+            run = id;
+            cnt = 0;
+            xmin = (uint32_t)px;
+          }
+          ++cnt;
+          xmax = (uint32_t)px;
+        }
+        if (b.depth) b.depth[o + k] = dep;
+        if (b.normals) {
+          uint16_t* d = b.normals + (o + k) * 3;
+          d[0] = (uint16_t)(n01 & 0xFFFFu);
+          d[1] = (uint16_t)(n01 >> 16);
+          d[2] = (uint16_t)n2;
+        }
+        if (b.points) {
+          float pt[3];
+          if (bg) pt[0] = pt[1] = pt[2] = __builtin_nanf("");
+          else unproject(b.cam + (size_t)f * kCamFloats, px, py, dep, pt);
+          float* d = b.points + (o + k) * 3;
+          d[0] = pt[0];
+          d[1] = pt[1];
+          d[2] = pt[2];
+        }
       }
+      flush_run();
+    }
+    if (pend) L.q.more = 1;          // (__syncthreads_or measured 16% slower here)
+    __syncthreads();
+    if (!L.q.more) break;
+  }
+  if (row_ok) {
+    uint32_t rgb[4];
+    int32_t ids[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long w = zrow[k];
+      rgb[k] = (uint32_t)w;
+      ids[k] = (int32_t)(w >> 32);
     }
     if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
-      if (b.normals) {   // 4 px x 3 halves = three 8-B words
-        uint2* d = reinterpret_cast<uint2*>(b.normals + o * 3);
-        d[0] = make_uint2(nrm[0][0], (nrm[0][1] & 0xFFFFu) | (nrm[1][0] << 16));
-        d[1] = make_uint2((nrm[1][0] >> 16) | (nrm[1][1] << 16), nrm[2][0]);
-        d[2] = make_uint2((nrm[2][1] & 0xFFFFu) | (nrm[3][0] << 16), (nrm[3][0] >> 16) | (nrm[3][1] << 16));
-      }
-      if (b.points) {    // 4 px x 3 floats = three 16-B words
-        float4* d = reinterpret_cast<float4*>(b.points + o * 3);
-        d[0] = make_float4(pts[0][0], pts[0][1], pts[0][2], pts[1][0]);
-        d[1] = make_float4(pts[1][1], pts[1][2], pts[2][0], pts[2][1]);
-        d[2] = make_float4(pts[2][2], pts[3][0], pts[3][1], pts[3][2]);
-      }
       if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(ids[0], ids[1], ids[2], ids[3]);
-      if (b.depth) *reinterpret_cast<float4*>(b.depth + o) = make_float4(dep[0], dep[1], dep[2], dep[3]);
       if (b.rgb) {
         uint32_t* d = reinterpret_cast<uint32_t*>(b.rgb + o * 3);
         d[0] = rgb[0] | (rgb[1] << 24);
@@ -1166,17 +1227,6 @@ __global__ __launch_bounds__(256) void k_raster(SceneDev s, BatchDev b) {
     } else {
       for (int k = 0; k < 4 && px0 + k < (int)s.W; ++k) {
         if (b.inst) b.inst[o + k] = ids[k];
-        if (b.depth) b.depth[o + k] = dep[k];
-        if (b.normals) {
-          b.normals[(o + k) * 3 + 0] = (uint16_t)(nrm[k][0] & 0xFFFFu);
-          b.normals[(o + k) * 3 + 1] = (uint16_t)(nrm[k][0] >> 16);
-          b.normals[(o + k) * 3 + 2] = (uint16_t)(nrm[k][1] & 0xFFFFu);
-        }
-        if (b.points) {
-          b.points[(o + k) * 3 + 0] = pts[k][0];
-          b.points[(o + k) * 3 + 1] = pts[k][1];
-          b.points[(o + k) * 3 + 2] = pts[k][2];
-        }
         if (b.rgb) {
           b.rgb[(o + k) * 3 + 0] = (uint8_t)(rgb[k] & 255u);
           b.rgb[(o + k) * 3 + 1] = (uint8_t)((rgb[k] >> 8) & 255u);
@@ -1343,11 +1393,9 @@ void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t block
   hipLaunchKernelGGL(k_bin, g, dim3(kBlock), 2 * s.n_tiles * sizeof(uint32_t), st, s, b);
 }
 
-void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st, int variant) {
+void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
   dim3 g(s.n_tiles, F);
-  // variant: 0 = production; 1 = owner-map level 2 (kept for A/B)
-  if (variant == 1) hipLaunchKernelGGL(k_raster<1>, g, dim3(kBlock), 0, st, s, b);
-  else hipLaunchKernelGGL(k_raster<0>, g, dim3(kBlock), 0, st, s, b);
+  hipLaunchKernelGGL(k_raster, g, dim3(kBlock), 0, st, s, b);
 }
 
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st) {

@@ -23,7 +23,7 @@ def load(d):
     return per
 
 
-def main(root, write_profile=False, workload="C3", frames_per_step=60):
+def main(root, write_profile=False, workload="C3", frames_per_launch=60):
     out = {}
     for sub in sorted(os.listdir(root)):
         p = os.path.join(root, sub)
@@ -40,7 +40,7 @@ def main(root, write_profile=False, workload="C3", frames_per_step=60):
     print(json.dumps(out, indent=1, sort_keys=True))
     if write_profile and "k_raster" in out and "hbm_bytes_per_launch" in out["k_raster"]:
         here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        prof = {"workload": workload, "frames_per_step": frames_per_step,
+        prof = {"workload": workload, "frames_per_launch": frames_per_launch,
                 "k_raster_bytes_per_launch": int(out["k_raster"]["hbm_bytes_per_launch"]),
                 "k_raster_fetch_size_kb": out["k_raster"]["FETCH_SIZE"],
                 "k_raster_write_size_kb": out["k_raster"]["WRITE_SIZE"],
