@@ -707,16 +707,22 @@ struct RasterCtx {
 //
 // Occupancy: k_raster is latency-bound (LDS and VMEM dependency chains), and
 // waves per SIMD are its lever (measured on C3: 3 waves +22% time vs 4, 5 waves
-// -8% vs 4).  Five 256-thread workgroups per CU need <= 32 KiB of LDS each
-// (176 staged records, 192 shade-table slots) and <= 96 VGPRs.
+// -8% vs 4).  Five 256-thread workgroups per CU need <= 31.5 KiB of LDS each
+// (168 staged records, 192 shade-table slots) and <= 96 VGPRs.
 #ifndef CSG_RASTER_FRAME_FAST
 #define CSG_RASTER_FRAME_FAST 0
 #endif
+#ifndef CSG_L1_BITMAP
+#define CSG_L1_BITMAP 1
+#endif
+#ifndef CSG_L2_BITMAP
+#define CSG_L2_BITMAP 1
+#endif
 #ifndef CSG_TILE_SWIZZLE
-#define CSG_TILE_SWIZZLE 0
+#define CSG_TILE_SWIZZLE 2
 #endif
 #ifndef CSG_STAGE
-#define CSG_STAGE 176
+#define CSG_STAGE 168
 #endif
 #ifndef CSG_WAVES
 #define CSG_WAVES 5             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
@@ -815,19 +821,31 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 }
 
 struct RasterLds {
-  RecImage img;                         // 28 KiB staged bin records
+  RecImage img;                         // staged bin records
+#if CSG_L1_BITMAP
+  uint32_t starts1[kStage];             // bit i: a staged record's rows start at level-1 item i
+  uint16_t before1[kStage + 1];         // records starting before item 32*d
+  uint32_t crec[kStage];                // compact record: slot | first item << 8
+#else
   uint32_t pre[kBlock + 1];             // row-item prefix per record
+#endif
   uint8_t row0[kBlock];                 // first tile row of each staged record | 0x80 if small
   uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
+#if CSG_L2_BITMAP
+  uint32_t starts[kBlock];              // bit i: a span starts at level-2 item i (<= 256 spans x 32 px)
+  uint16_t before[kBlock + 1];          // spans starting before item 32*d
+#else
   uint32_t pre2[kBlock + 1];            // pixel-item prefix per span
+#endif
   uint32_t wsum[kBlock / 64];
 };
 
 // Block-level two-level expansion of kStage-record batches.
 //   level 1: (record, row) items, one per thread -> exact row span
-//   level 2: (span, pixel) items; each finds its span by a 4-ary search over
-//            the span prefix (a per-item owner map measured slower: its LDS
-//            cost a workgroup per CU).
+//   level 2: (span, pixel) items
+// An item finds its record / span by a rank query over a bitmap of starts
+// (measured: -5.5% k_raster vs a 4-ary search over the prefix; a per-item
+// owner map cost a workgroup per CU in LDS).
 __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds& L, uint32_t beg,
                                              uint32_t end, const uint32_t* bins, const Rec* recs) {
   const int tid = threadIdx.x;
@@ -839,23 +857,47 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
       atomicAdd(&b.overflow[1], 1u);
       atomicAdd(&b.overflow[2], rows);
     }
+#if CSG_L1_BITMAP
+    // records with rows get compact indices; item -> record is a rank query
+    // over a bitmap of record starts (as for level 2 below)
+    if (tid < kStage) L.starts1[tid] = 0u;   // ordered before the atomics by the scan's barriers
+    if (tid == 0) L.before1[0] = 0;
+    uint32_t tot1p;
+    const uint32_t ex1p = block_excl_scan(rows | (rows ? 0x10000u : 0u), L.wsum, tot1p);
+    const uint32_t tot1 = tot1p & 0xFFFFu;
+    if (rows) {
+      const uint32_t ex1 = ex1p & 0xFFFFu, ci = ex1p >> 16, e_end = ex1 + rows;
+      L.crec[ci] = (uint32_t)tid | (ex1 << 8);
+      atomicOr(&L.starts1[ex1 >> 5], 1u << (ex1 & 31u));
+      if ((e_end & ~31u) > ex1) L.before1[e_end >> 5] = (uint16_t)(ci + 1u);
+    }
+#else
     uint32_t tot1;
     const uint32_t ex1 = block_excl_scan(rows, L.wsum, tot1);
     L.pre[tid] = ex1;
     if (tid == kBlock - 1) L.pre[kBlock] = ex1 + rows;
+#endif
     __syncthreads();
     for (uint32_t c1 = 0; c1 < ((b.dbg & 256u) ? 0u : tot1); c1 += kBlock) {
       const uint32_t j1 = c1 + tid;
       uint32_t w2 = 0, sp = 0;
       int xl = 0;
       if (j1 < tot1) {
+#if CSG_L1_BITMAP
+        const uint32_t w1 = L.starts1[j1 >> 5], nb1 = L.before1[j1 >> 5];
+        const uint32_t cr = L.crec[nb1 + (uint32_t)__popc(w1 & (0xFFFFFFFFu >> (31u - (j1 & 31u)))) - 1u];
+        const int k = (int)(cr & 255u);
+        const uint32_t first = cr >> 8;
+#else
         const int k = find_item(L.pre, j1);
+        const uint32_t first = L.pre[k];
+#endif
         const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
         const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
         const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
         const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTile - 1);
         const uint32_t r0b = L.row0[k];
-        const int ly = (int)(r0b & 31u) + (int)(j1 - L.pre[k]);
+        const int ly = (int)(r0b & 31u) + (int)(j1 - first);
         int xr;
         if (b.dbg & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
         else if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
@@ -869,6 +911,32 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         atomicAdd(&b.overflow[3], 1u);
         atomicAdd(&b.overflow[4], w2);
       }
+#if CSG_L2_BITMAP
+      // Non-empty spans get compact indices (one packed scan gives item
+      // offset and index).  Item -> span is then a rank query: a bitmap of
+      // span starts plus, per 32-item word, the spans starting before it (the
+      // one span crossing each word boundary writes it) -- two independent
+      // LDS reads and a popcount instead of a 4-step search.
+      L.starts[tid] = 0u;                 // ordered before the atomics by the scan's barriers
+      if (tid == 0) L.before[0] = 0;
+      uint32_t totp;
+      const uint32_t exp = block_excl_scan(w2 | (w2 ? 0x10000u : 0u), L.wsum, totp);
+      const uint32_t ex2 = exp & 0xFFFFu, tot2 = totp & 0xFFFFu;
+      if (w2) {
+        const uint32_t ci = exp >> 16, e_end = ex2 + w2;
+        L.span[ci] = sp | ((ex2 - (uint32_t)xl + 32u) << 16);
+        atomicOr(&L.starts[ex2 >> 5], 1u << (ex2 & 31u));
+        if ((e_end & ~31u) > ex2) L.before[e_end >> 5] = (uint16_t)(ci + 1u);   // word boundary inside
+      }
+      __syncthreads();
+      for (uint32_t j = tid; j < ((b.dbg & 8u) ? 0u : tot2); j += kBlock) {
+        const uint32_t w = L.starts[j >> 5], nb = L.before[j >> 5];
+        const uint32_t rank = nb + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31u - (j & 31u))));
+        const uint32_t spj = L.span[rank - 1u];
+        fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
+      }
+      __syncthreads();
+#else
       uint32_t tot2;
       const uint32_t ex2 = block_excl_scan(w2, L.wsum, tot2);
       L.span[tid] = sp | ((ex2 - (uint32_t)xl + 32u) << 16);
@@ -880,6 +948,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
+#endif
     }
   }
 }
@@ -1025,8 +1094,9 @@ struct ResolveLds {
 };
 
 // The resolve's LDS aliases the raster loop's in a union inside k_raster.
+// (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4.)
 static_assert((sizeof(RasterLds) > sizeof(ResolveLds) ? sizeof(RasterLds) : sizeof(ResolveLds)) + kTilePix * 8 <=
-                  (CSG_WAVES >= 5 ? 32768u : 40960u),
+                  (CSG_WAVES >= 5 ? 32256u : 40960u),
               "k_raster LDS must allow CSG_WAVES workgroups per CU");
 
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
@@ -1048,11 +1118,12 @@ __device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
 // square share one L2, so a record binned to several of them is fetched once,
 // while all XCDs keep working side by side on the same part of the frame.
 // Blocks past the frame's edge (odd tile counts) return at once.
+constexpr uint32_t kSq = CSG_TILE_SWIZZLE > 0 ? CSG_TILE_SWIZZLE : 1;   // square edge in tiles
 __device__ __forceinline__ bool swizzled_tile(uint32_t v, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tile) {
-  const uint32_t sqx = (tiles_x + 1) >> 1, sqy = (tiles_y + 1) >> 1;
-  const uint32_t sq = (v >> 5) * 8u + (v & 7u), j = (v >> 3) & 3u;
+  const uint32_t sqx = (tiles_x + kSq - 1) / kSq, sqy = (tiles_y + kSq - 1) / kSq;
+  const uint32_t sq = (v / (8u * kSq * kSq)) * 8u + (v & 7u), j = (v >> 3) % (kSq * kSq);
   if (sq >= sqx * sqy) return false;
-  const uint32_t tx = (sq % sqx) * 2u + (j & 1u), ty = (sq / sqx) * 2u + (j >> 1);
+  const uint32_t tx = (sq % sqx) * kSq + (j % kSq), ty = (sq / sqx) * kSq + (j / kSq);
   if (tx >= tiles_x || ty >= tiles_y) return false;
   tile = ty * tiles_x + tx;
   return true;
@@ -1491,8 +1562,8 @@ void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t
 #if CSG_RASTER_FRAME_FAST
   dim3 g(F, s.n_tiles);
 #elif CSG_TILE_SWIZZLE
-  const uint32_t squares = ((s.tiles_x + 1) / 2) * ((s.tiles_y + 1) / 2);
-  dim3 g(32 * ((squares + 7) / 8), F);
+  const uint32_t squares = ((s.tiles_x + kSq - 1) / kSq) * ((s.tiles_y + kSq - 1) / kSq);
+  dim3 g(8 * kSq * kSq * ((squares + 7) / 8), F);
 #else
   dim3 g(s.n_tiles, F);
 #endif
