@@ -706,9 +706,11 @@ struct RasterCtx {
 // 3 A2 B0 B1 B2 | 4 C0 C1 C2 invdet | 5 uv0-3 | 6 uv4 uv5 atex_wh athr.
 //
 // Occupancy: k_raster is latency-bound (LDS and VMEM dependency chains), and
-// waves per SIMD are its lever (measured on C3: 3 waves +22% time vs 4, 5 waves
-// -8% vs 4).  Five 256-thread workgroups per CU need <= 31.5 KiB of LDS each
-// (168 staged records, 192 shade-table slots) and <= 96 VGPRs.
+// waves per SIMD are its lever (measured on C3 against 4 waves: 3 waves +22%
+// time, 5 waves -8%, 6 waves a further -5%; 7 and 8 waves lose again to the
+// smaller batches and shade tables they need).  Six 256-thread workgroups per
+// CU need <= 26 KiB of LDS each (128 staged records, 128 shade-table slots)
+// and <= 80 VGPRs.
 #ifndef CSG_RASTER_FRAME_FAST
 #define CSG_RASTER_FRAME_FAST 0
 #endif
@@ -722,10 +724,10 @@ struct RasterCtx {
 #define CSG_TILE_SWIZZLE 2
 #endif
 #ifndef CSG_STAGE
-#define CSG_STAGE 168
+#define CSG_STAGE 128
 #endif
 #ifndef CSG_WAVES
-#define CSG_WAVES 5             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
+#define CSG_WAVES 6             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
 #endif
 #if CSG_WAVES > 0
 #define CSG_RASTER_ATTR __attribute__((amdgpu_waves_per_eu(CSG_WAVES, CSG_WAVES)))
@@ -1051,15 +1053,18 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
 }
 
 // Depth, instance id and RGB of pixel (px, py) covered by entry e.
-__device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry& e, int px, int py,
+// The homogeneous evaluation is needed only for the depth (when depth or
+// points are requested) and for texture coordinates.
+__device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry& e, int px, int py, bool need_depth,
                                             uint32_t& rgb_out, int32_t& id_out, float& depth_out) {
-  float ev[3], ssum, invw;
-  hom_eval(e.A, e.B, e.C, e.invdet, px, py, ev, ssum, invw);
-  depth_out = 1.0f / invw;
+  const bool textured = e.tex >= 0 && !(s.dbg & 4096u);   // 4096: ablation only, no texture fetch
+  float ev[3], ssum = 0.0f, invw = 0.0f;
+  if (need_depth || textured) hom_eval(e.A, e.B, e.C, e.invdet, px, py, ev, ssum, invw);
+  depth_out = need_depth ? 1.0f / invw : INFINITY;
   id_out = e.label;
   int base[3] = {(int)(e.base & 255u), (int)((e.base >> 8) & 255u), (int)((e.base >> 16) & 255u)};
   int alb[3];
-  if (e.tex >= 0 && !(s.dbg & 4096u)) {   // 4096: ablation only, no texture fetch
+  if (textured) {
     float u, v;
     int c[4];
     interp_uv(ev, ssum, e.uv, u, v);
@@ -1081,7 +1086,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
 // triangles in an open-addressing table of kShadeSlots, each set up once by
 // one thread, then read by every pixel that shows it.
 #ifndef CSG_SHADE_SLOTS
-#define CSG_SHADE_SLOTS 192
+#define CSG_SHADE_SLOTS 128
 #endif
 constexpr uint32_t kShadeSlots = CSG_SHADE_SLOTS;   // <= kBlock (one setup thread per slot)
 static_assert(kShadeSlots <= (uint32_t)kBlock && kShadeSlots < 255u, "one setup thread per slot; 8-bit slot ids");
@@ -1094,9 +1099,10 @@ struct ResolveLds {
 };
 
 // The resolve's LDS aliases the raster loop's in a union inside k_raster.
-// (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4.)
+// (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4;
+// 26,656 B keeps 6.)
 static_assert((sizeof(RasterLds) > sizeof(ResolveLds) ? sizeof(RasterLds) : sizeof(ResolveLds)) + kTilePix * 8 <=
-                  (CSG_WAVES >= 5 ? 32256u : 40960u),
+                  (CSG_WAVES >= 7 ? 22528u : CSG_WAVES == 6 ? 26700u : CSG_WAVES == 5 ? 32256u : 40960u),
               "k_raster LDS must allow CSG_WAVES workgroups per CU");
 
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
@@ -1267,7 +1273,11 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   const size_t npx = (size_t)s.W * s.H;
   const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
   const uint32_t bgmask = row_ok ? (~pend & 15u) : 0u;   // background pixels inside the frame
-  for (bool first = true;; first = false) {
+  const bool need_depth = b.depth || b.points;
+  // One round; returns whether any pixel of the tile is left.  The first
+  // round is peeled off (called outside the loop) so the compiler does not
+  // hoist per-pixel invariants across the setup phase, where they would spill.
+  auto round = [&](const bool first) __attribute__((always_inline)) -> bool {
     if ((uint32_t)tid < kShadeSlots) L.q.keys[tid] = kNoAlpha;
     __syncthreads();
     // every thread has read the previous round's flag (it reached this
@@ -1309,20 +1319,33 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     }
     __syncthreads();
     if (row_ok) {
+      // pixel coordinates laundered through an empty asm: everything derived
+      // from them is computed here, not hoisted across the setup phase above
+      // (it would be live there and spill)
+      int qx0 = px0, qy = py;
+      asm volatile("" : "+v"(qx0), "+v"(qy));
+      const size_t qo = (size_t)f * npx + (size_t)qy * s.W + qx0;
       int32_t run = -1;              // label stats, one set of LDS atomics per run of equal labels
       uint32_t cnt = 0, xmin = 0, xmax = 0;
       auto flush_run = [&]() {
         if (run >= 0 && (uint32_t)run < nl) {
           atomicAdd(&lstat[0][run], cnt);
           atomicMin(&lstat[1][run], xmin);
-          atomicMin(&lstat[2][run], (uint32_t)py);
+          atomicMin(&lstat[2][run], (uint32_t)qy);
           atomicMax(&lstat[3][run], xmax);
-          atomicMax(&lstat[4][run], (uint32_t)py);
+          atomicMax(&lstat[4][run], (uint32_t)qy);
+        } else if (run >= 0 && b.stats && (uint32_t)run < b.n_labels) {   // beyond the LDS table
+          uint32_t* st = b.stats + ((size_t)f * b.n_labels + (uint32_t)run) * 5;
+          atomicAdd(&st[0], cnt);
+          atomicMin(&st[1], xmin);
+          atomicMin(&st[2], (uint32_t)qy);
+          atomicMax(&st[3], xmax);
+          atomicMax(&st[4], (uint32_t)qy);
         }
       };
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int px = px0 + k;
+        const int px = qx0 + k;
         const uint32_t sl = (slots >> (8 * k)) & 0xFFu;
         // background pixels are written in the first round; the optional
         // outputs are stored per pixel so their values are never live long
@@ -1334,7 +1357,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
           const ShadeEntry& e = L.q.tab[sl];
           uint32_t rgb;
           int32_t id;
-          shade_pixel(s, e, px, py, rgb, id, dep);
+          shade_pixel(s, e, px, qy, need_depth, rgb, id, dep);
           n01 = e.n01;
           n2 = e.n2;
           zrow[k] = (unsigned long long)rgb | ((unsigned long long)(uint32_t)id << 32);
@@ -1348,9 +1371,9 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
           ++cnt;
           xmax = (uint32_t)px;
         }
-        if (b.depth) b.depth[o + k] = dep;
+        if (b.depth) b.depth[qo + k] = dep;
         if (b.normals) {
-          uint16_t* d = b.normals + (o + k) * 3;
+          uint16_t* d = b.normals + (qo + k) * 3;
           d[0] = (uint16_t)(n01 & 0xFFFFu);
           d[1] = (uint16_t)(n01 >> 16);
           d[2] = (uint16_t)n2;
@@ -1358,8 +1381,8 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
         if (b.points) {
           float pt[3];
           if (bg) pt[0] = pt[1] = pt[2] = __builtin_nanf("");
-          else unproject(b.cam + (size_t)f * kCamFloats, px, py, dep, pt);
-          float* d = b.points + (o + k) * 3;
+          else unproject(b.cam + (size_t)f * kCamFloats, px, qy, dep, pt);
+          float* d = b.points + (qo + k) * 3;
           d[0] = pt[0];
           d[1] = pt[1];
           d[2] = pt[2];
@@ -1369,7 +1392,12 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     }
     if (pend) L.q.more = 1;          // (__syncthreads_or measured 16% slower here)
     __syncthreads();
-    if (!L.q.more) break;
+    return L.q.more != 0;
+  };
+  if (round(true)) {
+#pragma clang loop unroll(disable)
+    while (round(false)) {
+    }
   }
   if (row_ok) {
     uint32_t rgb[4];

@@ -98,7 +98,7 @@ def pack_scene(scene: Scene, instance_models: Optional[List[np.ndarray]] = None)
     counts = np.array([scene.meshes[i.mesh].n_tris for i in scene.instances], np.int64)
     base = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint32)
     amb, sun, d, sky = light_constants(scene.light)
-    n_labels = max([o.inst_idx for o in scene.objects] + [-1]) + 1
+    n_labels = max([o.inst_idx for o in scene.objects] + [i.inst_idx for i in scene.instances] + [-1]) + 1
     return PackedScene(
         positions=np.concatenate(pos) if pos else np.zeros((0, 3), np.float32),
         tris=np.concatenate(tri) if tri else np.zeros((0, 3), np.uint32),
