@@ -242,6 +242,9 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   if (uvs.empty()) uvs.assign(2, 0.f);
   std::vector<MatDesc> mats(n_materials);
   for (uint32_t k = 0; k < n_materials; ++k) {
+    if (materials[k].alpha_threshold > 255u)
+      return c->fail(CSG_ERR_INVALID, "material %u: alpha_threshold %u > 255 (alpha is 8-bit)", k,
+                     materials[k].alpha_threshold);
     memcpy(mats[k].base, materials[k].base_color, 4);
     mats[k].texture = materials[k].texture;
     mats[k].alpha_test = materials[k].alpha_test;

@@ -80,7 +80,7 @@ typedef struct {
   uint8_t base_color[4];     /* sRGB u8 albedo multiplier (alpha unused) */
   int32_t texture;           /* texture id or -1 */
   uint32_t alpha_test;       /* 1: discard fragments with texture alpha <= threshold */
-  uint32_t alpha_threshold;
+  uint32_t alpha_threshold;  /* 0..255 (alpha is 8-bit) */
 } csg_material;
 
 typedef struct {
