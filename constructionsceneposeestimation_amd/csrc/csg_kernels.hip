@@ -1328,6 +1328,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       int32_t run = -1;              // label stats, one set of LDS atomics per run of equal labels
       uint32_t cnt = 0, xmin = 0, xmax = 0;
       auto flush_run = [&]() {
+        if (b.dbg & 16384u) return;   // ablation only: no label stats
         if (run >= 0 && (uint32_t)run < nl) {
           atomicAdd(&lstat[0][run], cnt);
           atomicMin(&lstat[1][run], xmin);
