@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames-per-step", type=int, default=120)
+    ap.add_argument("--frames-per-step", type=int, default=240)
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--frames-per-launch", type=int, default=0, help="frames per kernel chain (0 = library default)")
     ap.add_argument("--seed", type=int, default=0)
