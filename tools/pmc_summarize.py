@@ -50,4 +50,8 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], "--write-profile" in sys.argv)
+    fpl = 240
+    for a in sys.argv[2:]:
+        if a.startswith("--frames-per-launch="):
+            fpl = int(a.split("=", 1)[1])
+    main(sys.argv[1], "--write-profile" in sys.argv, frames_per_launch=fpl)
