@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=384, help="frames rendered by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pcie-steps", type=int, default=3, help="batches timed with host outputs (0 = skip)")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -86,6 +87,9 @@ def main():
         st = wl.epoch(e)
         r.set_instance_transforms(set_of[e], st.models)
         r.set_keypoints(set_of[e], st.keypoints)
+        if st.dr is not None:                      # C4: per-epoch lighting and texture DR
+            r.set_dr_light(set_of[e], st.dr.light)
+            r.set_dr_textures(set_of[e], st.dr.textures)
     views, projs = wl.frame_params(fids)
     frames = make_frames(views, projs, [set_of[f // 10] for f in fids], fids)
     frames_dev = torch.from_numpy(frames.view(np.uint8).copy()).to(dev)
@@ -147,6 +151,33 @@ def main():
     stage_ms = {k: tm[k] / K for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")}
     b_geom = wl.scene.authored_bytes()
 
+    # ---- PCIe-inclusive rate (rank 0, N=1 only; never `value`): the same
+    # batches with the outputs copied to pinned host buffers by the library
+    pcie = None
+    if rank == 0 and world == 1 and args.pcie_steps > 0:
+        try:
+            import ctypes as C
+            from constructionsceneposeestimation_amd import _lib
+            h_rgb = torch.empty((F, H, Wd, 3), dtype=torch.uint8, pin_memory=True)
+            h_inst = torch.empty((F, H, Wd), dtype=torch.int32, pin_memory=True)
+            h_uv = torch.empty((F, Kp, 2), dtype=torch.float32, pin_memory=True)
+            h_vis = torch.empty((F, Kp), dtype=torch.int32, pin_memory=True)
+            o = _lib.Outputs(h_rgb.data_ptr(), h_inst.data_ptr(), None, h_uv.data_ptr(), h_vis.data_ptr(), None,
+                             r.n_labels, 0, None, None)
+            hframes = np.ascontiguousarray(frames[:F])
+            r._check(r.lib.csg_render_batch_async(r.ctx, hframes.ctypes.data, F, 0, C.byref(o), None), "pcie")
+            r.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.pcie_steps):
+                r._check(r.lib.csg_render_batch_async(r.ctx, hframes.ctypes.data, F, 0, C.byref(o), None), "pcie")
+            r.synchronize()
+            dt = time.perf_counter() - t1
+            pcie = {"value": round(args.pcie_steps * F / dt, 2), "unit": "frames/s",
+                    "note": f"outputs (RGB8 + int32 ids + keypoints, {H * Wd * 7 / 1e6:.1f} MB/frame) copied to "
+                            f"pinned host memory inside the timed region; {args.pcie_steps} batches of {F}"}
+        except Exception as e:  # the extra figure must never break the bench line
+            log(f"pcie-inclusive measurement failed: {e}")
+
     # ---- CPU baseline (rank 0, N=1 only): the oracle on a bounded sample ----
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -185,6 +216,7 @@ def main():
                          "kernel": "k_raster", "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": round(raster_ms, 4)},
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "frame_roofline": {"B_frame": b_geom + b_tex + npx * 7,
                                "frac": round(value / world * (b_geom + b_tex + npx * 7) / (HBM_PEAK_GBS * 1e9), 5)},
