@@ -229,3 +229,31 @@ def test_many_labels_stats(cone):
     seen = np.unique(ora["instance"])
     assert (seen >= 256).sum() > 10, "test scene must show labels past the LDS table"
     assert np.array_equal(gpu["inst_stats"][0], ora["inst_stats"])
+
+
+def test_coplanar_ties_across_meshes_and_instances():
+    """Coplanar duplicates tie on depth everywhere: the (depth, uid) key must
+    pick the lower instance even when its mesh lies later in the triangle
+    soup (the GPU's uid carries the soup index, the spec's the mesh-relative
+    index; both order (instance, triangle) the same way)."""
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd.scene.model import Instance, Material, Mesh, Scene, SceneObject
+    W, H = 96, 64
+    v = np.array([[-5, -5, 0], [5, -5, 0], [5, 5, 0], [-5, 5, 0]], np.float32)
+    t = np.array([[0, 1, 2], [0, 2, 3]], np.uint32)
+    s = Scene()
+    s.materials = [Material("grey", np.array([0.5, 0.5, 0.5])), Material("red", np.array([0.9, 0.1, 0.1]))]
+    no_uv = (np.zeros((0, 2), np.float32), np.zeros((0, 3), np.uint32))
+    s.meshes = [Mesh("a", v, t, *no_uv, 0), Mesh("b", v, t[::-1].copy(), *no_uv, 1)]
+    # instance 0 uses mesh b (later in the soup), instances 1 and 2 mesh a
+    s.instances = [Instance(1, np.eye(4), 0, 0, np.eye(4)), Instance(0, np.eye(4), 1, 1, np.eye(4)),
+                   Instance(0, np.eye(4), 2, 2, np.eye(4))]
+    s.objects = [SceneObject(f"/q{k}", "fence", 2, k) for k in range(3)]
+    C = np.eye(4)
+    C[:3, 3] = [0.4, -0.3, 4.0]
+    V, P = cm.view_matrix(C), cm.Intrinsics(W, H).pixel_projection()
+    ora = _oracle(s, W, H).render(V, P)
+    with _renderer(s, W, H, 1) as r:
+        gpu = r.render(_frames(V[None], P[None]))
+    assert (ora["instance"] == 0).all()
+    _assert_same(gpu, ora, 0)
