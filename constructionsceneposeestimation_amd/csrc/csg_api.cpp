@@ -81,6 +81,8 @@ struct csg_ctx {
   bool tex_dirty = true;
   DevBuf<uint8_t> texels;
   DevBuf<uint32_t> aquad;
+  DevBuf<uint32_t> acls;                // alpha-test class of each alpha quad (see build_alpha_classes)
+  std::vector<int> acls_thr;            // per texture: the threshold acls was built for
   DevBuf<TexDesc> texd;
   LightDev light{{0.26f, 0.29f, 0.34f}, {0.78f, 0.78f, 0.78f}, {0.7071f, 0.f, 0.7071f},
                  191u | (217u << 8) | (255u << 16)};   // default (csg_set_light)
@@ -193,6 +195,7 @@ void csg_destroy(csg_ctx* c) {
   c->chunks.release();
   c->texels.release();
   c->aquad.release();
+  c->acls.release();
   c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
   c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
   c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
@@ -410,14 +413,57 @@ int csg_set_keypoints(csg_ctx* c, uint32_t set_id, const float* pts, uint32_t n)
   return CSG_OK;
 }
 
+// Alpha-test class of every alpha quad (2 bits, 16 per word, indexed like the
+// alpha-quad image): 0 = all four alphas <= the threshold (the bilinear value
+// is too, the test fails whatever the weights), 1 = all four above it (passes),
+// 3 = mixed (k_raster loads the quad and filters).  The threshold is that of
+// the alpha-tested materials bound to the texture in any transform set; a
+// texture used with two thresholds (or none) stays "mixed" everywhere, so the
+// class map never changes a result, it only spares most tests the 4-B quad
+// load from the much larger quad image.
+static int build_alpha_classes(csg_ctx* c, const std::vector<TexDesc>& td, size_t total, bool tex_changed) {
+  std::vector<int> thr(c->textures.size(), -1);   // -1 unused, -2 conflicting
+  for (const MatDesc& m : c->h_set_mats) {
+    if (!m.alpha_test || m.texture < 0 || (size_t)m.texture >= thr.size()) continue;
+    int& t = thr[m.texture];
+    if (t == -1) t = (int)m.alpha_threshold;
+    else if (t != (int)m.alpha_threshold) t = -2;
+  }
+  if (!tex_changed && c->acls.p && thr == c->acls_thr) return CSG_OK;   // same textures, same thresholds
+  c->acls_thr = thr;
+  std::vector<uint32_t> cls((total + 15) / 16 + 1, 0xFFFFFFFFu);
+  for (size_t k = 0; k < c->textures.size(); ++k) {
+    const HostTexture& t = c->textures[k];
+    if (!t.present || thr[k] < 0) continue;
+    const uint32_t th = (uint32_t)thr[k];
+    for (uint32_t y = 0; y < t.h; ++y)
+      for (uint32_t x = 0; x < t.w; ++x) {
+        const uint32_t x1 = x + 1 == t.w ? 0 : x + 1, y1 = y + 1 == t.h ? 0 : y + 1;
+        auto a = [&](uint32_t xx, uint32_t yy) { return (uint32_t)t.rgba[((size_t)yy * t.w + xx) * 4 + 3]; };
+        const uint32_t q[4] = {a(x, y), a(x1, y), a(x, y1), a(x1, y1)};
+        const uint32_t mn = std::min(std::min(q[0], q[1]), std::min(q[2], q[3]));
+        const uint32_t mx = std::max(std::max(q[0], q[1]), std::max(q[2], q[3]));
+        const uint32_t cl = mx <= th ? 0u : mn > th ? 1u : 3u;
+        const size_t i = (size_t)td[k].offset + (size_t)y * t.w + x;
+        cls[i >> 4] = (cls[i >> 4] & ~(3u << (2 * (i & 15)))) | (cl << (2 * (i & 15)));
+      }
+  }
+  HIP_TRY(c, c->acls.alloc(cls.size()));
+  HIP_TRY(c, hipMemcpy(c->acls.p, cls.data(), cls.size() * 4, hipMemcpyHostToDevice));
+  return CSG_OK;
+}
+
 static int sync_scene_state(csg_ctx* c) {
+  const uint32_t n_sets = (uint32_t)c->set_valid.size();
+  const bool tex_changed = c->tex_dirty;
+  const bool cls_dirty = c->tex_dirty || c->dr_dirty || c->n_table_sets != n_sets || !c->acls.p;
+  std::vector<TexDesc> td(c->textures.size());
+  size_t total = 0;
+  for (size_t k = 0; k < c->textures.size(); ++k) {
+    td[k] = TexDesc{(uint32_t)total, c->textures[k].w, c->textures[k].h, 0};
+    total += (size_t)c->textures[k].w * c->textures[k].h;
+  }
   if (c->tex_dirty) {
-    std::vector<TexDesc> td(c->textures.size());
-    size_t total = 0;
-    for (size_t k = 0; k < c->textures.size(); ++k) {
-      td[k] = TexDesc{(uint32_t)total, c->textures[k].w, c->textures[k].h, 0};
-      total += (size_t)c->textures[k].w * c->textures[k].h;
-    }
     HIP_TRY(c, c->texels.alloc(std::max<size_t>(total * 4, 4)));
     HIP_TRY(c, c->aquad.alloc(std::max<size_t>(total, 1)));
     HIP_TRY(c, c->texd.alloc(std::max<size_t>(td.size(), 1)));
@@ -441,7 +487,6 @@ static int sync_scene_state(csg_ctx* c) {
     c->tex_dirty = false;
   }
   // per-set material and light tables (every set that has transforms)
-  const uint32_t n_sets = (uint32_t)c->set_valid.size();
   if (c->dr_dirty || c->n_table_sets != n_sets) {
     std::vector<MatDesc> sm((size_t)n_sets * c->n_materials);
     std::vector<LightDev> sl(n_sets);
@@ -461,6 +506,10 @@ static int sync_scene_state(csg_ctx* c) {
     if (!sl.empty()) HIP_TRY(c, hipMemcpy(c->lights.p, sl.data(), sl.size() * sizeof(LightDev), hipMemcpyHostToDevice));
     c->n_table_sets = n_sets;
     c->dr_dirty = false;
+  }
+  if (cls_dirty) {
+    const int rc = build_alpha_classes(c, td, total, tex_changed);
+    if (rc) return rc;
   }
   for (size_t k = 0; k < c->h_set_mats.size(); ++k) {
     const int t = c->h_set_mats[k].texture;
@@ -516,7 +565,7 @@ static int ensure_work(csg_ctx* c) {
 static SceneDev scene_dev(const csg_ctx* c) {
   SceneDev s{};
   s.tri_pos = c->tri_pos.p; s.tri_uv = c->tri_uv.p; s.inst = c->inst.p;
-  s.texd = c->texd.p; s.texels = c->texels.p; s.aquad = c->aquad.p; s.n_inst = c->n_inst;
+  s.texd = c->texd.p; s.texels = c->texels.p; s.aquad = c->aquad.p; s.acls = c->acls.p; s.n_inst = c->n_inst;
   s.W = c->cfg.width; s.H = c->cfg.height;
   s.tiles_x = c->tiles_x; s.tiles_y = c->tiles_y; s.n_tiles = c->n_tiles;
   s.near_clip = c->cfg.near_clip; s.far_clip = c->cfg.far_clip;
@@ -686,7 +735,8 @@ int csg_synchronize(csg_ctx* c) {
   if ((c->dbg & 512u) && c->overflow.p) {   // profiling counters, cumulative since the work buffers were sized
     uint32_t ctr[16];
     HIP_TRY(c, hipMemcpy(ctr, c->overflow.p, sizeof(ctr), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u\n", ctr[1], ctr[2], ctr[3], ctr[4]);
+    fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u alpha_fail %u alpha_pass %u early_z %u\n",
+            ctr[1], ctr[2], ctr[3], ctr[4], ctr[5], ctr[6], ctr[7]);
   }
   if (ov)
     return c->fail(CSG_ERR_OVERFLOW, "work buffer overflow (flags %u): records_per_frame=%u bins_per_frame=%u", ov,

@@ -67,7 +67,8 @@ struct SceneDev {
   const InstDesc* inst;        // [I]
   const TexDesc* texd;
   const uint8_t* texels;        // RGBA8, all textures back to back (TexDesc.offset in texels)
-  const uint32_t* aquad;        // alpha quads, same indexing (see tex_alpha)
+  const uint32_t* aquad;        // alpha quads, same indexing (see alpha_pass)
+  const uint32_t* acls;         // 2-bit alpha-test class per alpha quad, 16 per word (see alpha_pass)
   uint32_t n_inst;
   uint32_t W, H, tiles_x, tiles_y, n_tiles;
   float near_clip, far_clip;

@@ -31,6 +31,13 @@
 
 namespace csg {
 
+#ifndef CSG_ALPHA_CLASS
+#define CSG_ALPHA_CLASS 1      // alpha tests decided by the 2-bit quad class where it can (see alpha_pass)
+#endif
+#ifndef CSG_SMALL_COVER
+#define CSG_SMALL_COVER 4      // records with at most N x N pixel centres get an exact cover test in k_setup (0: off)
+#endif
+
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr float kGuardPx = 1048576.0f;
 
@@ -140,19 +147,30 @@ __device__ __forceinline__ void tex_sample(const SceneDev& s, int tid, float u, 
   for (int c = 0; c < 4; ++c) out[c] = tex_channel(c00, c10, c01, c11, 8 * c, k.wx, k.wy);
 }
 
-// Alpha channel only (the alpha test), from the alpha-quad image: texel
-// (x, y) holds the alphas of (x,y), (x+1,y), (x,y+1), (x+1,y+1) (wrapped), so
-// the bilinear footprint is one 4-byte load.  `wh` = width | height << 16.
-__device__ __forceinline__ int tex_alpha(const uint32_t* aquad, uint32_t offset, uint32_t wh, float u, float v) {
+// The alpha test: bilinear alpha (8-bit weights, as tex_sample) > thr.
+// The alpha-quad image holds at texel (x, y) the alphas of (x,y), (x+1,y),
+// (x,y+1), (x+1,y+1) (wrapped), so the bilinear footprint is one 4-byte load.
+// First the 2-bit class of that quad (acls, 16 per word, 1/16 of the quad
+// image, so it stays in L2): all four alphas <= thr -> the filtered value is
+// too (weights sum to 65536 and the rounding cannot cross an integer), fail;
+// all four > thr -> pass; only mixed quads (~5% of a foliage card's texels)
+// load the quad and filter.  `wh` = width | height << 16.
+__device__ __forceinline__ bool alpha_pass(const uint32_t* aquad, const uint32_t* acls, uint32_t offset, uint32_t wh,
+                                           int thr, float u, float v) {
   const int tw = (int)(wh & 0xFFFFu), th = (int)(wh >> 16);
   float tu = u * (float)tw - 0.5f;
   float tv = (1.0f - v) * (float)th - 0.5f;
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
+  const uint32_t idx = offset + (uint32_t)(wrap_index(fv, th) * tw + wrap_index(fu, tw));
+#if CSG_ALPHA_CLASS
+  const uint32_t cl = (acls[idx >> 4] >> (2u * (idx & 15u))) & 3u;
+  if (cl != 3u) return cl != 0u;
+#endif
   const int wx = (int)((tu - fu) * 256.0f), wy = (int)((tv - fv) * 256.0f);
-  const uint32_t q = aquad[offset + (uint32_t)(wrap_index(fv, th) * tw + wrap_index(fu, tw))];
-  return bilerp8(q & 255u, (q >> 8) & 255u, (q >> 16) & 255u, q >> 24, wx, wy);
+  const uint32_t q = aquad[idx];
+  return bilerp8(q & 255u, (q >> 8) & 255u, (q >> 16) & 255u, q >> 24, wx, wy) > thr;
 }
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -303,6 +321,46 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
   px1 = min(px1, (int)s.W - 1);
   py1 = min(py1, (int)s.H - 1);
   if (px0 > px1 || py0 > py1) return false;
+#if CSG_SMALL_COVER
+  // Small records (at most NxN pixel centres in the box, vertex extent below
+  // 32 px): evaluate the spec's edge test at every centre of the box, drop the
+  // record if it covers none and shrink the box to the covered pixels.  The
+  // covered set is unchanged (so are the outputs); fewer, tighter records mean
+  // fewer record stores, bin entries and raster row items.  Exact in int32:
+  // |dx|, |dy| < 2^13 and every centre lies within the vertex extent.
+  constexpr int N = CSG_SMALL_COVER;
+  if (px1 - px0 < N && py1 - py0 < N && xmax - xmin < 8192 && ymax - ymin < 8192) {
+    const int32_t cx0 = px0 * 256 + 128, cy0 = py0 * 256 + 128;
+    const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+    int32_t e0[3], sx[3], sy[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const int32_t dx = x[eb[e]] - x[ea[e]], dy = y[eb[e]] - y[ea[e]];
+      const int32_t bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+      e0[e] = __mul24(dx, cy0 - y[ea[e]]) - __mul24(dy, cx0 - x[ea[e]]) + bias;
+      sx[e] = -dy * 256;
+      sy[e] = dx * 256;
+    }
+    const int nw = px1 - px0, nh = py1 - py0;
+    uint32_t cols = 0, rows = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        bool in = i <= nw && j <= nh;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) in &= e0[e] + sx[e] * i + sy[e] * j >= 0;
+        cols |= in ? 1u << i : 0u;
+        rows |= in ? 1u << j : 0u;
+      }
+    }
+    if (!cols) return false;
+    px1 = px0 + 31 - __clz(cols);
+    px0 += __ffs(cols) - 1;
+    py1 = py0 + 31 - __clz(rows);
+    py0 += __ffs(rows) - 1;
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < 3; ++k) { r.x[k] = x[k]; r.y[k] = y[k]; }
   r.px0 = (uint16_t)px0; r.py0 = (uint16_t)py0; r.px1 = (uint16_t)px1; r.py1 = (uint16_t)py1;
@@ -692,10 +750,12 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // ---------------------------------------------------------------------------
 struct RasterCtx {
   const uint32_t* aquad;
+  const uint32_t* acls;
   unsigned long long* zb;
   int ox, oy;
   float inv_near, inv_far;
   uint32_t dbg;
+  uint32_t* ctr;   // profiling counters (CSG_DEBUG 512 only)
 };
 
 // LDS image of up to kStage staged records as seven 16-B field groups (the Rec
@@ -755,13 +815,18 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
-  if (!(c.dbg & 16u) && key >= *z) return;
+  if (!(c.dbg & 16u) && key >= *z) {
+    if (c.dbg & 512u) atomicAdd(&c.ctr[7], 1u);   // profiling: early-z rejects
+    return;
+  }
   if (!(c.dbg & 4u) && g2.y != kNoAlpha) {
     const uint4 g5 = I.q[5][k], g6 = I.q[6][k];
     const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
     float u, v;
     interp_uv(e, ssum, uv, u, v);
-    if (!(tex_alpha(c.aquad, g2.y, g6.z, u, v) > (int)g6.w)) return;
+    const bool pass = alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)g6.w, u, v);
+    if (c.dbg & 512u) atomicAdd(&c.ctr[pass ? 6 : 5], 1u);   // profiling: alpha tests passed / failed
+    if (!pass) return;
   }
   atomicMin(z, key);
 }
@@ -1219,7 +1284,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
   const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
-  RasterCtx c{s.aquad, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg};
+  RasterCtx c{s.aquad, s.acls, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg, b.overflow};
   __syncthreads();
   raster_block(c, b, L.r, beg, end, bins, recs);
   __syncthreads();
