@@ -569,6 +569,7 @@ static SceneDev scene_dev(const csg_ctx* c) {
   s.W = c->cfg.width; s.H = c->cfg.height;
   s.tiles_x = c->tiles_x; s.tiles_y = c->tiles_y; s.n_tiles = c->n_tiles;
   s.near_clip = c->cfg.near_clip; s.far_clip = c->cfg.far_clip;
+  s.inv_near = 1.0f / c->cfg.near_clip; s.inv_far = 1.0f / c->cfg.far_clip;
   s.dbg = c->dbg;
   return s;
 }
@@ -735,8 +736,8 @@ int csg_synchronize(csg_ctx* c) {
   if ((c->dbg & 512u) && c->overflow.p) {   // profiling counters, cumulative since the work buffers were sized
     uint32_t ctr[16];
     HIP_TRY(c, hipMemcpy(ctr, c->overflow.p, sizeof(ctr), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u alpha_fail %u alpha_pass %u early_z %u\n",
-            ctr[1], ctr[2], ctr[3], ctr[4], ctr[5], ctr[6], ctr[7]);
+    fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u alpha_fail %u alpha_pass %u early_z %u "
+            "wide_rows %u\n", ctr[1], ctr[2], ctr[3], ctr[4], ctr[5], ctr[6], ctr[7], ctr[8]);
   }
   if (ov)
     return c->fail(CSG_ERR_OVERFLOW, "work buffer overflow (flags %u): records_per_frame=%u bins_per_frame=%u", ov,

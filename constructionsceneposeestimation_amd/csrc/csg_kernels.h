@@ -72,6 +72,7 @@ struct SceneDev {
   uint32_t n_inst;
   uint32_t W, H, tiles_x, tiles_y, n_tiles;
   float near_clip, far_clip;
+  float inv_near, inv_far;     // 1/near_clip, 1/far_clip (IEEE, computed on the host)
   uint32_t dbg;                // ablation switches (CSG_DEBUG; 0 in production)
 };
 

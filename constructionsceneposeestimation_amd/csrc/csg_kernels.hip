@@ -122,16 +122,24 @@ __device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {
   const int x0 = wrap_index(fu, tw), y0 = wrap_index(fv, th);
   const int x1 = (x0 + 1 == tw) ? 0 : x0 + 1;
   const int y1 = (y0 + 1 == th) ? 0 : y0 + 1;
-  t.i00 = (uint32_t)(y0 * tw + x0); t.i10 = (uint32_t)(y0 * tw + x1);
-  t.i01 = (uint32_t)(y1 * tw + x0); t.i11 = (uint32_t)(y1 * tw + x1);
+  const uint32_t r0 = __umul24((uint32_t)y0, (uint32_t)tw), r1 = __umul24((uint32_t)y1, (uint32_t)tw);
+  t.i00 = r0 + (uint32_t)x0; t.i10 = r0 + (uint32_t)x1;
+  t.i01 = r1 + (uint32_t)x0; t.i11 = r1 + (uint32_t)x1;
   return t;
 }
 
+// Operands are below 2^24 (channels <= 255, weights <= 256), so every
+// product is a full-rate 24-bit multiply (a plain int multiply here becomes
+// the quarter-rate v_mul_lo_u32).
 __device__ __forceinline__ int bilerp8(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, int wx, int wy) {
-  const int top = (int)c00 * (256 - wx) + (int)c10 * wx;
-  const int bot = (int)c01 * (256 - wx) + (int)c11 * wx;
-  return (top * (256 - wy) + bot * wy + 32768) >> 16;
+  const uint32_t ax = 256u - (uint32_t)wx, ay = 256u - (uint32_t)wy;
+  const uint32_t top = __umul24(c00, ax) + __umul24(c10, (uint32_t)wx);
+  const uint32_t bot = __umul24(c01, ax) + __umul24(c11, (uint32_t)wx);
+  return (int)((__umul24(top, ay) + __umul24(bot, (uint32_t)wy) + 32768u) >> 16);
 }
+
+// x / 255 for 0 <= x < 2^16 (exhaustively equal), one 24-bit multiply
+__device__ __forceinline__ int div255(uint32_t x) { return (int)(__umul24(x, 32897u) >> 23); }
 
 __device__ __forceinline__ int tex_channel(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, int sh, int wx,
                                            int wy) {
@@ -163,7 +171,7 @@ __device__ __forceinline__ bool alpha_pass(const uint32_t* aquad, const uint32_t
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
-  const uint32_t idx = offset + (uint32_t)(wrap_index(fv, th) * tw + wrap_index(fu, tw));
+  const uint32_t idx = offset + __umul24((uint32_t)wrap_index(fv, th), (uint32_t)tw) + (uint32_t)wrap_index(fu, tw);
 #if CSG_ALPHA_CLASS
   const uint32_t cl = (acls[idx >> 4] >> (2u * (idx & 15u))) & 3u;
   if (cl != 3u) return cl != 0u;
@@ -715,12 +723,12 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
     if constexpr (Small) c0[e] = __mul24(dx, cy - ay) + __mul24(dy, ax) + bias;
     else c0[e] = (int64_t)dx * (cy - ay) + (int64_t)dy * ax + bias;
     dys[e] = dy;
-    if (dy == 0) {
-      if (c0[e] < 0) hi = -1.0e30f;
-    } else {
-      const float t = __fdividef((float)c0[e], (float)dy);   // approximate: covered by the margin
-      if (dy > 0) hi = fminf(hi, t); else lo = fmaxf(lo, t);
-    }
+    // boundary of the edge on this row, approximate (rcp: ~2 ulp, far below
+    // the 1/16-px margin where it matters); branch-free (no divergence)
+    const float t = (float)c0[e] * __builtin_amdgcn_rcpf((float)dy);
+    hi = (dy > 0) ? fminf(hi, t) : hi;
+    lo = (dy < 0) ? fmaxf(lo, t) : lo;
+    hi = (dy == 0 && c0[e] < 0) ? -1.0e30f : hi;
   }
   const float l = fminf(fmaxf((lo - 128.0f) * (1.0f / 256.0f) - 0.0625f, (float)x0 - 1.0f), (float)x1 + 1.0f);
   const float h = fmaxf(fminf((hi - 128.0f) * (1.0f / 256.0f) + 0.0625f, (float)x1 + 1.0f), (float)x0 - 1.0f);
@@ -864,11 +872,15 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
     if (fx[k] >= sl && fx[k] <= sr) { ylo = fminf(ylo, fy[k]); yhi = fmaxf(yhi, fy[k]); }
     const int n = (k + 1) % 3;
     const float dxe = fx[n] - fx[k], dye = fy[n] - fy[k];
+    // 1/dxe: hardware reciprocal + one Newton step (<= ~1 ulp; the half-pixel
+    // widening below covers it), instead of two IEEE divisions per edge
+    const float r0 = __builtin_amdgcn_rcpf(dxe);
+    const float rdx = fmaf(fmaf(-dxe, r0, 1.0f), r0, r0);
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       const float xs = side ? sr : sl;
       if ((fx[k] - xs) * (fx[n] - xs) < 0.0f) {
-        const float yc = fy[k] + (xs - fx[k]) / dxe * dye;
+        const float yc = fy[k] + (xs - fx[k]) * rdx * dye;
         ylo = fminf(ylo, yc);
         yhi = fmaxf(yhi, yc);
       }
@@ -968,7 +980,10 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         int xr;
         if (b.dbg & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
         else if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
-        else row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
+        else {
+          if (b.dbg & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
+          row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
+        }
         if (xl <= xr) {
           w2 = (uint32_t)(xr - xl + 1);
           sp = (uint32_t)k | ((uint32_t)ly << 8);
@@ -1135,7 +1150,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
     interp_uv(ev, ssum, e.uv, u, v);
     tex_sample(s, e.tex, u, v, c);
 #pragma unroll
-    for (int z = 0; z < 3; ++z) alb[z] = (c[z] * base[z] + 127) / 255;
+    for (int z = 0; z < 3; ++z) alb[z] = div255(__umul24((uint32_t)c[z], (uint32_t)base[z]) + 127u);
   } else {
 #pragma unroll
     for (int z = 0; z < 3; ++z) alb[z] = base[z];
@@ -1143,7 +1158,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
   const int q[3] = {(int)(e.q01 & 0xFFFFu), (int)(e.q01 >> 16), (int)e.q2};
   uint32_t o = 0;
 #pragma unroll
-  for (int z = 0; z < 3; ++z) o |= (uint32_t)min((alb[z] * q[z] + 128) >> 8, 255) << (8 * z);
+  for (int z = 0; z < 3; ++z) o |= (uint32_t)min((int)((__umul24((uint32_t)alb[z], (uint32_t)q[z]) + 128u) >> 8), 255) << (8 * z);
   rgb_out = o;
 }
 
@@ -1284,7 +1299,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
   const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
-  RasterCtx c{s.aquad, s.acls, zb, ox, oy, 1.0f / s.near_clip, 1.0f / s.far_clip, b.dbg, b.overflow};
+  RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow};
   __syncthreads();
   raster_block(c, b, L.r, beg, end, bins, recs);
   __syncthreads();
