@@ -31,6 +31,10 @@
 
 namespace csg {
 
+#ifndef CSG_ABLATION
+#define CSG_ABLATION 0         // 1: honour the CSG_DEBUG ablation / profiling bits (tools/ablate.sh builds)
+#endif
+#define DBG(d) (CSG_ABLATION ? (d) : 0u)
 #ifndef CSG_ALPHA_CLASS
 #define CSG_ALPHA_CLASS 1      // alpha tests decided by the 2-bit quad class where it can (see alpha_pass)
 #endif
@@ -407,7 +411,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   const uint32_t f = blockIdx.x, chunk = blockIdx.y + blockIdx.z * gridDim.y;
   if (chunk >= n_chunks) return;
   const int tid = threadIdx.x, lane = tid & 63;
-  if (b.dbg & 32u) return;            // ablation: empty setup
+  if (DBG(b.dbg) & 32u) return;            // ablation: empty setup
   const Chunk& ch = chunks[chunk];   // read fields in place (a runtime-indexed copy would spill)
   const uint32_t i = ch.inst;
   const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     const bool cull = ((__ballot(out_n) & m8) == m8) || ((__ballot(out_f) & m8) == m8) ||
                       ((__ballot(out_l) & m8) == m8) || ((__ballot(out_r) & m8) == m8) ||
                       ((__ballot(out_t) & m8) == m8) || ((__ballot(out_b) & m8) == m8);
-    if (cull || (b.dbg & 64u)) return;   // identical in every wave of the block (64: ablation, cull all)
+    if (cull || (DBG(b.dbg) & 64u)) return;   // identical in every wave of the block (64: ablation, cull all)
   }
 
   Rec r0, r1;   // named, never runtime-indexed (a Rec[2] would live in scratch)
@@ -559,7 +563,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     store_rec(b.recs + (size_t)f * b.rec_cap + slot, rec);
     b.rect[(size_t)f * b.rec_cap + slot] = rec_tile_rect(rec);
   };
-  if (b.dbg & 128u) {   // ablation: no record stores
+  if (DBG(b.dbg) & 128u) {   // ablation: no record stores
     if (nrec == 3 && b.inst) b.inst[0] = r0.uid + r1.uid;
     return;
   }
@@ -823,17 +827,17 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
-  if (!(c.dbg & 16u) && key >= *z) {
-    if (c.dbg & 512u) atomicAdd(&c.ctr[7], 1u);   // profiling: early-z rejects
+  if (!(DBG(c.dbg) & 16u) && key >= *z) {
+    if (DBG(c.dbg) & 512u) atomicAdd(&c.ctr[7], 1u);   // profiling: early-z rejects
     return;
   }
-  if (!(c.dbg & 4u) && g2.y != kNoAlpha) {
+  if (!(DBG(c.dbg) & 4u) && g2.y != kNoAlpha) {
     const uint4 g5 = I.q[5][k], g6 = I.q[6][k];
     const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
     float u, v;
     interp_uv(e, ssum, uv, u, v);
     const bool pass = alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)g6.w, u, v);
-    if (c.dbg & 512u) atomicAdd(&c.ctr[pass ? 6 : 5], 1u);   // profiling: alpha tests passed / failed
+    if (DBG(c.dbg) & 512u) atomicAdd(&c.ctr[pass ? 6 : 5], 1u);   // profiling: alpha tests passed / failed
     if (!pass) return;
   }
   atomicMin(z, key);
@@ -932,7 +936,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
     uint32_t row0;
     const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
     L.row0[tid] = (uint8_t)row0;
-    if ((b.dbg & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
+    if ((DBG(b.dbg) & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
       atomicAdd(&b.overflow[1], 1u);
       atomicAdd(&b.overflow[2], rows);
     }
@@ -957,7 +961,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
     if (tid == kBlock - 1) L.pre[kBlock] = ex1 + rows;
 #endif
     __syncthreads();
-    for (uint32_t c1 = 0; c1 < ((b.dbg & 256u) ? 0u : tot1); c1 += kBlock) {
+    for (uint32_t c1 = 0; c1 < ((DBG(b.dbg) & 256u) ? 0u : tot1); c1 += kBlock) {
       const uint32_t j1 = c1 + tid;
       uint32_t w2 = 0, sp = 0;
       int xl = 0;
@@ -978,18 +982,18 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         const uint32_t r0b = L.row0[k];
         const int ly = (int)(r0b & 31u) + (int)(j1 - first);
         int xr;
-        if (b.dbg & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
-        else if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
+        if (DBG(b.dbg) & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
+        else if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
         else {
-          if (b.dbg & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
-          row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, b.dbg & 2048u);
+          if (DBG(b.dbg) & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
+          row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
         }
         if (xl <= xr) {
           w2 = (uint32_t)(xr - xl + 1);
           sp = (uint32_t)k | ((uint32_t)ly << 8);
         }
       }
-      if ((b.dbg & 512u) && w2) {      // non-empty spans, level-2 items
+      if ((DBG(b.dbg) & 512u) && w2) {      // non-empty spans, level-2 items
         atomicAdd(&b.overflow[3], 1u);
         atomicAdd(&b.overflow[4], w2);
       }
@@ -1011,7 +1015,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         if ((e_end & ~31u) > ex2) L.before[e_end >> 5] = (uint16_t)(ci + 1u);   // word boundary inside
       }
       __syncthreads();
-      for (uint32_t j = tid; j < ((b.dbg & 8u) ? 0u : tot2); j += kBlock) {
+      for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kBlock) {
         const uint32_t w = L.starts[j >> 5], nb = L.before[j >> 5];
         const uint32_t rank = nb + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31u - (j & 31u))));
         const uint32_t spj = L.span[rank - 1u];
@@ -1025,7 +1029,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
       L.pre2[tid] = ex2;
       if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
       __syncthreads();
-      for (uint32_t j = tid; j < ((b.dbg & 8u) ? 0u : tot2); j += kBlock) {
+      for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kBlock) {
         const uint32_t spj = L.span[find_item(L.pre2, j)];
         fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
@@ -1137,7 +1141,7 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
 // points are requested) and for texture coordinates.
 __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry& e, int px, int py, bool need_depth,
                                             uint32_t& rgb_out, int32_t& id_out, float& depth_out) {
-  const bool textured = e.tex >= 0 && !(s.dbg & 4096u);   // 4096: ablation only, no texture fetch
+  const bool textured = e.tex >= 0 && !(DBG(s.dbg) & 4096u);   // 4096: ablation only, no texture fetch
   float ev[3], ssum = 0.0f, invw = 0.0f;
   if (need_depth || textured) hom_eval(e.A, e.B, e.C, e.invdet, px, py, ev, ssum, invw);
   depth_out = need_depth ? 1.0f / invw : INFINITY;
@@ -1291,8 +1295,8 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
   const uint32_t beg = min(toff[tile], b.bin_cap);
-  const uint32_t end = (b.dbg & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
-  if (beg == end && !(b.dbg & 2u)) {   // nothing binned here: background only
+  const uint32_t end = (DBG(b.dbg) & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
+  if (beg == end && !(DBG(b.dbg) & 2u)) {   // nothing binned here: background only
     empty_tile(s, b, f, tile, ox, oy);
     return;
   }
@@ -1304,7 +1308,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   raster_block(c, b, L.r, beg, end, bins, recs);
   __syncthreads();
 
-  if (b.dbg & 1u) {   // ablation: keep the raster loop alive, skip the resolve
+  if (DBG(b.dbg) & 1u) {   // ablation: keep the raster loop alive, skip the resolve
     if (tid == 0 && zb[0] == 0ull && b.inst) b.inst[0] = 0;
     return;
   }
@@ -1389,7 +1393,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       const uint32_t u = (uint32_t)tid < kShadeSlots ? L.q.keys[tid] : kNoAlpha;
       if (u != kNoAlpha) {
         ShadeEntry& e = L.q.tab[tid];
-        if (b.dbg & 8192u) {   // ablation only: no triangle setup (garbage shading)
+        if (DBG(b.dbg) & 8192u) {   // ablation only: no triangle setup (garbage shading)
           e = ShadeEntry{};
           e.invdet = 1.0f; e.tex = -1; e.label = 0;
         } else {
@@ -1408,7 +1412,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       int32_t run = -1;              // label stats, one set of LDS atomics per run of equal labels
       uint32_t cnt = 0, xmin = 0, xmax = 0;
       auto flush_run = [&]() {
-        if (b.dbg & 16384u) return;   // ablation only: no label stats
+        if (DBG(b.dbg) & 16384u) return;   // ablation only: no label stats
         if (run >= 0 && (uint32_t)run < nl) {
           atomicAdd(&lstat[0][run], cnt);
           atomicMin(&lstat[1][run], xmin);
