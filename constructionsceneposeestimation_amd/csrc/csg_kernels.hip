@@ -396,10 +396,20 @@ __device__ __forceinline__ uint32_t rect_area(uint32_t rc) {
   return (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
 }
 
+// q / w for q < 2^24, 1 <= w <= 256: float reciprocal estimate (off by at
+// most one), then one exact correction (no integer division sequence)
+__device__ __forceinline__ uint32_t small_div(uint32_t q, uint32_t w) {
+  uint32_t d = (uint32_t)((float)q * __builtin_amdgcn_rcpf((float)w));
+  const uint32_t p = __umul24(d, w);
+  d = p > q ? d - 1u : (p + w <= q ? d + 1u : d);
+  return d;
+}
+
 __device__ __forceinline__ uint32_t rect_tile(uint32_t rc, uint32_t q, uint32_t tiles_x) {
   const uint32_t tx0 = rc & 255u, ty0 = (rc >> 8) & 255u, tx1 = (rc >> 16) & 255u;
   const uint32_t w = tx1 - tx0 + 1;
-  return (ty0 + q / w) * tiles_x + tx0 + q % w;
+  const uint32_t r = small_div(q, w);
+  return __umul24(ty0 + r, tiles_x) + tx0 + (q - __umul24(r, w));
 }
 
 // Grid: x = frame (fast), (y, z) = chunk.  Consecutive workgroups take the
@@ -523,10 +533,12 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
           nq = (code == 1 || code == 2 || code == 4) ? 3 : 4;
         }
         auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
+          // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c)
           float su[3], sv[3];
-          su[0] = a.x / a.w; sv[0] = a.y / a.w;
-          su[1] = bb.x / bb.w; sv[1] = bb.y / bb.w;
-          su[2] = cc.x / cc.w; sv[2] = cc.y / cc.w;
+          const float ra = 1.0f / a.w, rb = 1.0f / bb.w, rc = 1.0f / cc.w;
+          su[0] = a.x * ra; sv[0] = a.y * ra;
+          su[1] = bb.x * rb; sv[1] = bb.y * rb;
+          su[2] = cc.x * rc; sv[2] = cc.y * rc;
           Rec rr;
           if (make_rec(s, su, sv, rr)) {
             rr.uid = uid;

@@ -318,7 +318,11 @@ int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float
       const int all_in = v[0].w >= near && v[1].w >= near && v[2].w >= near;
       if (all_in) {
         float su[3], sv[3];
-        for (int k = 0; k < 3; ++k) { su[k] = v[k].x / v[k].w; sv[k] = v[k].y / v[k].w; }
+        for (int k = 0; k < 3; ++k) {   /* spec 3: one reciprocal per vertex, u = X * (1/W) */
+          const float rw = 1.0f / v[k].w;
+          su[k] = v[k].x * rw;
+          sv[k] = v[k].y * rw;
+        }
         raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st);
       } else {
         /* Sutherland-Hodgman against W >= near, edges v0->v1, v1->v2, v2->v0 */
@@ -341,7 +345,11 @@ int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float
         for (int f = 1; f + 1 < nq; ++f) {
           const cv3 tri3[3] = {q[0], q[f], q[f + 1]};
           float su[3], sv[3];
-          for (int k = 0; k < 3; ++k) { su[k] = tri3[k].x / tri3[k].w; sv[k] = tri3[k].y / tri3[k].w; }
+          for (int k = 0; k < 3; ++k) {
+            const float rw = 1.0f / tri3[k].w;
+            su[k] = tri3[k].x * rw;
+            sv[k] = tri3[k].y * rw;
+          }
           raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st);
         }
       }
