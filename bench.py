@@ -140,14 +140,19 @@ def main():
     bytes_per_launch = int(round(frames_per_launch * (b_out + b_tex)))
     raster_ms = tm["ms_raster"] / launches
     achieved = bytes_per_launch / (raster_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = valu = None
     if os.path.exists(args.profile_json):
         try:
             pj = json.load(open(args.profile_json))
             if pj.get("workload") == args.workload and pj.get("frames_per_launch") == frames_per_launch:
                 traffic = pj.get("k_raster_bytes_per_launch")
+                if pj.get("k_raster_valu_busy") is not None:
+                    valu = {"busy": round(pj["k_raster_valu_busy"], 3),
+                            "lane_util": round(pj.get("k_raster_valu_lane_util") or 0.0, 3),
+                            "note": "the kernel's actual limiter: VALU issue (rocprofv3 SQ_ACTIVE_INST_VALU, "
+                                    "profiles/pmc_traffic.json)"}
         except Exception:
-            traffic = None
+            traffic = valu = None
     stage_ms = {k: tm[k] / K for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")}
     b_geom = wl.scene.authored_bytes()
 
@@ -214,7 +219,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "k_raster", "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": round(raster_ms, 4)},
+                         "avg_launch_ms": round(raster_ms, 4), "valu": valu},
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},

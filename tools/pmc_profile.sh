@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=${ROUND:-r01}
-ARGS=${BENCH_ARGS:---steps 6 --warmup 1 --cpu-sample 0}
+ARGS=${BENCH_ARGS:---steps 6 --warmup 1 --cpu-sample 0 --pcie-steps 0}
 OUT=gpurun_out/pmc_$R
 mkdir -p $OUT
 run() {  # name counters...
@@ -14,13 +14,14 @@ run() {  # name counters...
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o pmc -- python3 bench.py $ARGS > $OUT/$name.json 2> $OUT/$name.err
 }
 rc=0
-for p in ${PASSES:-fetch write sq sq2 tcc}; do
+for p in ${PASSES:-fetch write sq sq2 tcc valu}; do
   case $p in
     fetch) run fetch FETCH_SIZE ;;
     write) run write WRITE_SIZE ;;
     sq) run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY ;;
     sq2) run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM GRBM_GUI_ACTIVE SQ_BUSY_CYCLES ;;
     tcc) run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum ;;
+    valu) run valu SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE ;;
   esac
   rc=$?
   [ $rc -ne 0 ] && break

@@ -12,6 +12,9 @@ import os
 import sys
 from collections import defaultdict
 
+N_SIMD = 256 * 4    # MI355X: 256 CUs x 4 SIMDs
+N_XCD = 8
+
 
 def load(d):
     per = defaultdict(lambda: defaultdict(list))
@@ -37,6 +40,13 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
     for k, o in out.items():
         if "FETCH_SIZE" in o and "WRITE_SIZE" in o:
             o["hbm_bytes_per_launch"] = o["FETCH_SIZE"] * 1024 * 2 + o["WRITE_SIZE"] * 1024
+        if "SQ_ACTIVE_INST_VALU" in o and "GRBM_GUI_ACTIVE" in o and o["GRBM_GUI_ACTIVE"] > 0:
+            # VALU issue utilisation: SQ_ACTIVE_INST_VALU counts quad-cycles (one wave64 VALU
+            # instruction = one quad-cycle of its SIMD), summed over the chip's 1,024 SIMDs;
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+            o["valu_busy"] = o["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / (o["GRBM_GUI_ACTIVE"] / N_XCD)
+            if "SQ_THREAD_CYCLES_VALU" in o and o["SQ_ACTIVE_INST_VALU"] > 0:
+                o["valu_lane_util"] = o["SQ_THREAD_CYCLES_VALU"] / (o["SQ_ACTIVE_INST_VALU"] * 64)
     print(json.dumps(out, indent=1, sort_keys=True))
     if write_profile and "k_raster" in out and "hbm_bytes_per_launch" in out["k_raster"]:
         here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -45,6 +55,8 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
                 "k_raster_fetch_size_kb": out["k_raster"]["FETCH_SIZE"],
                 "k_raster_write_size_kb": out["k_raster"]["WRITE_SIZE"],
                 "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1; KB=1024 B",
+                "k_raster_valu_busy": out["k_raster"].get("valu_busy"),
+                "k_raster_valu_lane_util": out["k_raster"].get("valu_lane_util"),
                 "source": os.path.basename(os.path.normpath(root))}
         json.dump(prof, open(os.path.join(here, "profiles", "pmc_traffic.json"), "w"), indent=1)
 
