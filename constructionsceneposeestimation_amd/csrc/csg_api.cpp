@@ -747,16 +747,33 @@ int csg_synchronize(csg_ctx* c) {
 
 int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out) {
   if (!c) return CSG_ERR_INVALID;
-  for (int attempt = 0; attempt < 4; ++attempt) {
+  for (int attempt = 0; attempt < 6; ++attempt) {
     int rc = csg_render_batch_async(c, frames, n_frames, 0, out, nullptr);
     if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     uint32_t ov = 0;
     HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
     if (!ov) return CSG_OK;
-    // grow the overflowed capacity and re-render (results are a pure function of inputs)
-    if (ov & 1u) c->rec_cap = (uint32_t)std::min<uint64_t>(2ull * c->rec_cap, 0x7FFFFFFFull);
-    if (ov & 2u) c->bin_cap = (uint32_t)std::min<uint64_t>(2ull * c->bin_cap, 0x7FFFFFFFull);
+    // grow the overflowed capacity and re-render (results are a pure function
+    // of inputs): at least double it, or size it from the last launch chain's
+    // counters (records counted past the cap; bin totals of the records kept)
+    uint32_t need_rec = 0, need_bin = 0;
+    if (c->last_F) {
+      std::vector<uint32_t> cnt((size_t)c->last_F * kCounterStride);
+      HIP_TRY(c, hipMemcpy(cnt.data(), c->rec_count.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> off((size_t)c->last_F * (c->n_tiles + 1));
+      HIP_TRY(c, hipMemcpy(off.data(), c->tile_off.p, off.size() * 4, hipMemcpyDeviceToHost));
+      for (uint32_t f = 0; f < c->last_F; ++f) {
+        need_rec = std::max(need_rec, cnt[(size_t)f * kCounterStride]);
+        need_bin = std::max(need_bin, off[(size_t)f * (c->n_tiles + 1) + c->n_tiles]);
+      }
+    }
+    auto grow = [](uint32_t cap, uint32_t need) {
+      return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * cap, need + need / 8ull + 1024ull), 0x7FFFFFFFull);
+    };
+    if (ov & 1u) c->rec_cap = grow(c->rec_cap, need_rec);
+    if (ov & 2u) c->bin_cap = grow(c->bin_cap, need_bin);
+    if (ov & 1u) c->bin_cap = grow(c->bin_cap, 0);   // more records: more bin entries too
     c->work_frames = 0;
   }
   return c->fail(CSG_ERR_OVERFLOW, "work buffers overflowed after growth");

@@ -35,6 +35,12 @@ namespace csg {
 #define CSG_ABLATION 0         // 1: honour the CSG_DEBUG ablation / profiling bits (tools/ablate.sh builds)
 #endif
 #define DBG(d) (CSG_ABLATION ? (d) : 0u)
+#ifndef CSG_HASH_XOR
+#define CSG_HASH_XOR 0         // shade-table hash: 1 = xor-fold, 0 = multiplicative (measured faster)
+#endif
+#ifndef CSG_OPAQUE_DIRECT
+#define CSG_OPAQUE_DIRECT 1    // opaque fragments go straight to ds_min_u64 (see fragment)
+#endif
 #ifndef CSG_ALPHA_CLASS
 #define CSG_ALPHA_CLASS 1      // alpha tests decided by the 2-bit quad class where it can (see alpha_pass)
 #endif
@@ -114,16 +120,20 @@ __device__ __forceinline__ int wrap_index(float fu, int n) {
   return (int)r;
 }
 
-__device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {
+__device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {   // tw, th <= 16384
   float tu = u * (float)tw - 0.5f;
   float tv = (1.0f - v) * (float)th - 0.5f;
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
   TexTap t;
-  t.wx = (int)((tu - fu) * 256.0f);
-  t.wy = (int)((tv - fv) * 256.0f);
-  const int x0 = wrap_index(fu, tw), y0 = wrap_index(fv, th);
+  // tu - fu is exact and in [0, 1), so the weights are in [0, 255] and the
+  // wrapped indices below 16384 (upload limit): the masks change no value,
+  // they let the compiler use full-rate 24-bit multiplies
+  t.wx = (int)((tu - fu) * 256.0f) & 255;
+  t.wy = (int)((tv - fv) * 256.0f) & 255;
+  tw &= 0x7FFF;
+  const int x0 = wrap_index(fu, tw) & 0x3FFF, y0 = wrap_index(fv, th) & 0x3FFF;
   const int x1 = (x0 + 1 == tw) ? 0 : x0 + 1;
   const int y1 = (y0 + 1 == th) ? 0 : y0 + 1;
   const uint32_t r0 = __umul24((uint32_t)y0, (uint32_t)tw), r1 = __umul24((uint32_t)y1, (uint32_t)tw);
@@ -175,12 +185,13 @@ __device__ __forceinline__ bool alpha_pass(const uint32_t* aquad, const uint32_t
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
-  const uint32_t idx = offset + __umul24((uint32_t)wrap_index(fv, th), (uint32_t)tw) + (uint32_t)wrap_index(fu, tw);
+  const uint32_t idx = offset + __umul24((uint32_t)wrap_index(fv, th) & 0x3FFFu, (uint32_t)tw & 0x7FFFu) +
+                       ((uint32_t)wrap_index(fu, tw) & 0x3FFFu);   // (masks: see tex_taps)
 #if CSG_ALPHA_CLASS
   const uint32_t cl = (acls[idx >> 4] >> (2u * (idx & 15u))) & 3u;
   if (cl != 3u) return cl != 0u;
 #endif
-  const int wx = (int)((tu - fu) * 256.0f), wy = (int)((tv - fv) * 256.0f);
+  const int wx = (int)((tu - fu) * 256.0f) & 255, wy = (int)((tv - fv) * 256.0f) & 255;
   const uint32_t q = aquad[idx];
   return bilerp8(q & 255u, (q >> 8) & 255u, (q >> 16) & 255u, q >> 24, wx, wy) > thr;
 }
@@ -839,6 +850,14 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
+#if CSG_OPAQUE_DIRECT
+  // Without an alpha test the ds_min_u64 is the depth test: no early-z read,
+  // compare and branch (a losing key leaves the word unchanged).
+  if (g2.y == kNoAlpha && !(DBG(c.dbg) & 512u)) {
+    atomicMin(z, key);
+    return;
+  }
+#endif
   if (!(DBG(c.dbg) & 16u) && key >= *z) {
     if (DBG(c.dbg) & 512u) atomicAdd(&c.ctr[7], 1u);   // profiling: early-z rejects
     return;
@@ -1203,7 +1222,13 @@ static_assert((sizeof(RasterLds) > sizeof(ResolveLds) ? sizeof(RasterLds) : size
 
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
 __device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
+#if CSG_HASH_XOR
+  // [0, kShadeSlots): xor-fold of the uid (shifts only)
+  static_assert((kShadeSlots & (kShadeSlots - 1)) == 0, "power-of-two table");
+  const uint32_t h = (uid ^ (uid >> 7) ^ (uid >> 14) ^ (uid >> 21)) & (kShadeSlots - 1u);
+#else
   const uint32_t h = __umulhi(uid * 2654435761u, kShadeSlots);   // [0, kShadeSlots)
+#endif
 #pragma clang loop vectorize(disable) unroll(disable)
   for (int p = 0; p < kShadeProbes; ++p) {
     uint32_t idx = h + (uint32_t)p;
@@ -1356,19 +1381,24 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   const int px0 = ox + lx0;
   unsigned long long* zrow = &zb[ly * kTile + lx0];
   uint32_t pend = 0;                 // bit k: pixel k still to shade
+  uint32_t inmask = 0;               // bit k: pixel k lies inside the frame
   {
     const uint32_t sky = b.lights[b.frames[f].xform_set].sky & 0xFFFFFFu;
     const unsigned long long bgword = (unsigned long long)sky | (0xFFFFFFFFull << 32);   // id -1
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool in = row_ok && px0 + k < (int)s.W;
+      inmask |= in ? 1u << k : 0u;
       if (in && zrow[k] != kEmptyKey) pend |= 1u << k;
       else zrow[k] = bgword;         // background (or outside the frame)
     }
   }
   const size_t npx = (size_t)s.W * s.H;
   const size_t o = (size_t)f * npx + (size_t)py * s.W + px0;
-  const uint32_t bgmask = row_ok ? (~pend & 15u) : 0u;   // background pixels inside the frame
+  // background pixels inside the frame (a pixel past the right edge would
+  // address the next row's first pixels: per-pixel depth / normal / point
+  // stores must not see it)
+  const uint32_t bgmask = inmask & ~pend;
   const bool need_depth = b.depth || b.points;
   // One round; returns whether any pixel of the tile is left.  The first
   // round is peeled off (called outside the loop) so the compiler does not

@@ -153,7 +153,10 @@ int csg_set_keypoints(csg_ctx* ctx, uint32_t set_id, const float* pts_world, uin
 int csg_set_dr_light(csg_ctx* ctx, uint32_t set_id, const csg_light* light);
 int csg_set_dr_textures(csg_ctx* ctx, uint32_t set_id, const int32_t* texture_per_material, uint32_t n);
 
-/* Render n_frames (<= max_frames) frames; synchronous. */
+/* Render n_frames (<= max_frames) frames; synchronous.  A work buffer that
+ * overflows (records or bin entries past the configured caps) is grown from
+ * the device counters and the batch rendered again, up to 6 attempts; the
+ * results do not depend on the caps. */
 int csg_render_batch(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out);
 /* Same, enqueued on `stream` (a hipStream_t, NULL = context stream); frames
  * may be a device pointer when frames_on_device = 1.  Returns after enqueue. */
