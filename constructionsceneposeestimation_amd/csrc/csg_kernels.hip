@@ -35,6 +35,9 @@ namespace csg {
 #define CSG_ABLATION 0         // 1: honour the CSG_DEBUG ablation / profiling bits (tools/ablate.sh builds)
 #endif
 #define DBG(d) (CSG_ABLATION ? (d) : 0u)
+#ifndef CSG_SPAN_NOWALK
+#define CSG_SPAN_NOWALK 1      // row spans: exact walk only for boundaries within 1/64 px of a pixel centre
+#endif
 #ifndef CSG_HASH_XOR
 #define CSG_HASH_XOR 0         // shade-table hash: 1 = xor-fold, 0 = multiplicative (measured faster)
 #endif
@@ -757,10 +760,29 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
     lo = (dy < 0) ? fmaxf(lo, t) : lo;
     hi = (dy == 0 && c0[e] < 0) ? -1.0e30f : hi;
   }
+#if CSG_SPAN_NOWALK
+  // Near the strip the float boundaries are within ~1e-5 px of the exact ones
+  // (tile-relative values below 2^14 units, ~2^-22 relative error).  An end
+  // whose boundary lies farther than kEps from every pixel centre is exact as
+  // computed: every left edge is at least kEps left of xl, every right edge at
+  // least kEps right of xr.  Only a boundary within kEps of a centre (through
+  // it: the top-left bias decides) is walked with the exact test.
+  constexpr float kEps = 1.0f / 64.0f;
+  const float lc = (lo - 128.0f) * (1.0f / 256.0f), hc = (hi - 128.0f) * (1.0f / 256.0f);
+  const float lcc = fminf(fmaxf(lc, (float)x0 - 1.0f), (float)x1 + 1.0f);
+  const float hcc = fmaxf(fminf(hc, (float)x1 + 1.0f), (float)x0 - 1.0f);
+  xl = max((int)ceilf(lcc - kEps), x0);
+  xr = min((int)floorf(hcc + kEps), x1);
+  const float fl = lcc - floorf(lcc), fh = hcc - floorf(hcc);
+  const bool walk_l = lc > (float)x0 - 0.5f && lc < (float)x1 + 0.5f && (fl <= kEps || fl >= 1.0f - kEps);
+  const bool walk_r = hc > (float)x0 - 0.5f && hc < (float)x1 + 0.5f && (fh <= kEps || fh >= 1.0f - kEps);
+#else
   const float l = fminf(fmaxf((lo - 128.0f) * (1.0f / 256.0f) - 0.0625f, (float)x0 - 1.0f), (float)x1 + 1.0f);
   const float h = fmaxf(fminf((hi - 128.0f) * (1.0f / 256.0f) + 0.0625f, (float)x1 + 1.0f), (float)x0 - 1.0f);
   xl = max((int)ceilf(l), x0);
   xr = min((int)floorf(h), x1);
+  const bool walk_l = true, walk_r = true;
+#endif
   if (no_exact) return;   // ablation only (CSG_DEBUG 2048): superset span
   auto covers = [&](int lx) {
     const int32_t cx = lx * 256 + 128;
@@ -774,10 +796,14 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
   };
   // normally zero or one step: keep the loops scalar (the loop vectorizer
   // otherwise evaluates eight speculative steps per trip)
+  if (walk_l) {
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-  while (xl <= xr && !covers(xl)) ++xl;
+    while (xl <= xr && !covers(xl)) ++xl;
+  }
+  if (walk_r) {
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-  while (xr >= xl && !covers(xr)) --xr;
+    while (xr >= xl && !covers(xr)) --xr;
+  }
 }
 
 // ---------------------------------------------------------------------------
