@@ -35,6 +35,9 @@ namespace csg {
 #define CSG_ABLATION 0         // 1: honour the CSG_DEBUG ablation / profiling bits (tools/ablate.sh builds)
 #endif
 #define DBG(d) (CSG_ABLATION ? (d) : 0u)
+#ifndef CSG_TIGHT_ROWS
+#define CSG_TIGHT_ROWS 1       // staged row range widened by 1/16 px (not 1/2) for records near the tile
+#endif
 #ifndef CSG_SPAN_NOWALK
 #define CSG_SPAN_NOWALK 1      // row spans: exact walk only for boundaries within 1/64 px of a pixel centre
 #endif
@@ -948,14 +951,22 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
     }
   }
   if (!(ylo <= yhi)) return 0u;
-  const int r0 = (int)ceilf((ylo - 128.0f - 128.0f) * (1.0f / 256.0f));
-  const int r1 = (int)floorf((yhi - 128.0f + 128.0f) * (1.0f / 256.0f));
-  y0 = max(y0, oy + r0);
-  y1 = min(y1, oy + r1);
   bool small = true;
 #pragma unroll
   for (int k = 0; k < 3; ++k)
     small &= abs(X[k] - ox * 256) < (1 << 14) && abs(Y[k] - oy * 256) < (1 << 14);
+#if CSG_TIGHT_ROWS
+  // Vertices within 64 px of the tile: every value above is below 2^16 units
+  // and off by < 0.01 units, so a 1/16-px widening suffices (half a pixel
+  // otherwise added about one empty row per record and tile).
+  const float wid = small ? 16.0f : 128.0f;
+#else
+  const float wid = 128.0f;
+#endif
+  const int r0 = (int)ceilf((ylo - 128.0f - wid) * (1.0f / 256.0f));
+  const int r1 = (int)floorf((yhi - 128.0f + wid) * (1.0f / 256.0f));
+  y0 = max(y0, oy + r0);
+  y1 = min(y1, oy + r1);
   row0 = (uint32_t)(y0 - oy) | (small ? 0x80u : 0u);
   return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
