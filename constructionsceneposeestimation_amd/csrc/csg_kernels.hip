@@ -497,67 +497,81 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
       ot &= v[k].y < 0.0f;
       ob &= v[k].y > Hf * v[k].w;
     }
-    Hom h;
     if (!(on | of | ol | orr | ot | ob)) {
-      hom_setup(v, h);
-      if (h.ok) {
-        const MatDesc mat = b.mats[(size_t)b.frames[f].xform_set * b.n_mat + m.material];
-        float uv[6] = {0, 0, 0, 0, 0, 0};
-        if (mat.alpha_test && m.has_uv) {
-          const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
+      const uint32_t uid = (i << kUidShift) | t;
+      // Sutherland-Hodgman against W >= near over edges v0->v1, v1->v2, v2->v0
+      // (each edge emits [start vertex if inside][intersection if crossing]),
+      // written as a closed-form case table on the inside mask so the polygon
+      // stays in registers.
+      Cv3 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[2];
+      int nq = 3;
+      const bool in0 = v[0].w >= nearc, in1 = v[1].w >= nearc, in2 = v[2].w >= nearc;
+      if (!(in0 && in1 && in2)) {
+        auto cross_pt = [&](const Cv3& a, const Cv3& bb) {
+          const float tt = (nearc - a.w) / (bb.w - a.w);
+          Cv3 rr;
+          rr.x = a.x + tt * (bb.x - a.x);
+          rr.y = a.y + tt * (bb.y - a.y);
+          rr.w = nearc;
+          return rr;
+        };
+        auto sel = [](bool c, const Cv3& a, const Cv3& bb) {
+          Cv3 rr;
+          rr.x = c ? a.x : bb.x;
+          rr.y = c ? a.y : bb.y;
+          rr.w = c ? a.w : bb.w;
+          return rr;
+        };
+        const Cv3 I01 = cross_pt(v[0], v[1]), I12 = cross_pt(v[1], v[2]), I20 = cross_pt(v[2], v[0]);
+        const int code = (int)in0 | ((int)in1 << 1) | ((int)in2 << 2);
+        // code: 1 -> v0 I01 I20 | 2 -> I01 v1 I12 | 4 -> I12 v2 I20
+        //       3 -> v0 v1 I12 I20 | 6 -> I01 v1 v2 I20 | 5 -> v0 I01 I12 v2
+        q0 = sel(code == 2 || code == 6, I01, sel(code == 4, I12, v[0]));
+        q1 = sel(code == 1 || code == 5, I01, sel(code == 4, v[2], v[1]));
+        q2 = sel(code == 1 || code == 4, I20, sel(code == 6, v[2], I12));
+        q3 = sel(code == 3 || code == 6, I20, v[2]);
+        nq = (code == 1 || code == 2 || code == 4) ? 3 : 4;
+      }
+      auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
+        // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c)
+        float su[3], sv[3];
+        const float ra = 1.0f / a.w, rb = 1.0f / bb.w, rc = 1.0f / cc.w;
+        su[0] = a.x * ra; sv[0] = a.y * ra;
+        su[1] = bb.x * rb; sv[1] = bb.y * rb;
+        su[2] = cc.x * rc; sv[2] = cc.y * rc;
+        Rec rr;
+        if (make_rec(s, su, sv, rr)) {
+          if (nrec == 0) r0 = rr; else r1 = rr;
+          ++nrec;
+        }
+      };
+      if (nq >= 3) emit_tri(q0, q1, q2);
+      if (nq >= 4) emit_tri(q0, q2, q3);
+      // A record exists iff det != 0 and the screen test passes, in either
+      // order: the homogeneous setup, its IEEE reciprocal and the material
+      // loads are spent only on the few triangles that cover a pixel centre
+      // (about one in five of those that pass the frustum test).
+      if (nrec > 0) {
+        Hom h;
+        hom_setup(v, h);
+        if (!h.ok) {
+          nrec = 0;
+        } else {
+          const MatDesc mat = b.mats[(size_t)b.frames[f].xform_set * b.n_mat + m.material];
+          float uv[6] = {0, 0, 0, 0, 0, 0};
+          if (mat.alpha_test && m.has_uv) {
+            const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
 #pragma unroll
-          for (int k = 0; k < 6; ++k) uv[k] = tu[k];
-        }
-        uint32_t atex = kNoAlpha, atex_wh = 0, athr = 0;
-        if (mat.alpha_test && mat.texture >= 0) {
-          const TexDesc td = s.texd[mat.texture];
-          atex = td.offset;
-          atex_wh = td.width | (td.height << 16);
-          athr = mat.alpha_threshold;
-        }
-        const uint32_t uid = (i << kUidShift) | t;
-        // Sutherland-Hodgman against W >= near over edges v0->v1, v1->v2, v2->v0
-        // (each edge emits [start vertex if inside][intersection if crossing]),
-        // written as a closed-form case table on the inside mask so the polygon
-        // stays in registers.
-        Cv3 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[2];
-        int nq = 3;
-        const bool in0 = v[0].w >= nearc, in1 = v[1].w >= nearc, in2 = v[2].w >= nearc;
-        if (!(in0 && in1 && in2)) {
-          auto cross_pt = [&](const Cv3& a, const Cv3& bb) {
-            const float tt = (nearc - a.w) / (bb.w - a.w);
-            Cv3 rr;
-            rr.x = a.x + tt * (bb.x - a.x);
-            rr.y = a.y + tt * (bb.y - a.y);
-            rr.w = nearc;
-            return rr;
-          };
-          auto sel = [](bool c, const Cv3& a, const Cv3& bb) {
-            Cv3 rr;
-            rr.x = c ? a.x : bb.x;
-            rr.y = c ? a.y : bb.y;
-            rr.w = c ? a.w : bb.w;
-            return rr;
-          };
-          const Cv3 I01 = cross_pt(v[0], v[1]), I12 = cross_pt(v[1], v[2]), I20 = cross_pt(v[2], v[0]);
-          const int code = (int)in0 | ((int)in1 << 1) | ((int)in2 << 2);
-          // code: 1 -> v0 I01 I20 | 2 -> I01 v1 I12 | 4 -> I12 v2 I20
-          //       3 -> v0 v1 I12 I20 | 6 -> I01 v1 v2 I20 | 5 -> v0 I01 I12 v2
-          q0 = sel(code == 2 || code == 6, I01, sel(code == 4, I12, v[0]));
-          q1 = sel(code == 1 || code == 5, I01, sel(code == 4, v[2], v[1]));
-          q2 = sel(code == 1 || code == 4, I20, sel(code == 6, v[2], I12));
-          q3 = sel(code == 3 || code == 6, I20, v[2]);
-          nq = (code == 1 || code == 2 || code == 4) ? 3 : 4;
-        }
-        auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
-          // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c)
-          float su[3], sv[3];
-          const float ra = 1.0f / a.w, rb = 1.0f / bb.w, rc = 1.0f / cc.w;
-          su[0] = a.x * ra; sv[0] = a.y * ra;
-          su[1] = bb.x * rb; sv[1] = bb.y * rb;
-          su[2] = cc.x * rc; sv[2] = cc.y * rc;
-          Rec rr;
-          if (make_rec(s, su, sv, rr)) {
+            for (int k = 0; k < 6; ++k) uv[k] = tu[k];
+          }
+          uint32_t atex = kNoAlpha, atex_wh = 0, athr = 0;
+          if (mat.alpha_test && mat.texture >= 0) {
+            const TexDesc td = s.texd[mat.texture];
+            atex = td.offset;
+            atex_wh = td.width | (td.height << 16);
+            athr = mat.alpha_threshold;
+          }
+          auto fill = [&](Rec& rr) {
             rr.uid = uid;
             rr.atex = atex;
             rr.atex_wh = atex_wh;
@@ -567,12 +581,10 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
             rr.invdet = h.invdet;
 #pragma unroll
             for (int k = 0; k < 6; ++k) rr.uv[k] = uv[k];
-            if (nrec == 0) r0 = rr; else r1 = rr;
-            ++nrec;
-          }
-        };
-        if (nq >= 3) emit_tri(q0, q1, q2);
-        if (nq >= 4) emit_tri(q0, q2, q3);
+          };
+          fill(r0);
+          if (nrec > 1) fill(r1);
+        }
       }
     }
   }
