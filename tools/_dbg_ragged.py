@@ -1,3 +1,4 @@
+"""Debug aid: GPU vs oracle mismatch counts for two world2 poses at a given size (args: W H records_per_frame)."""
 import os, sys
 import numpy as np
 sys.path.insert(0, os.getcwd())
