@@ -1411,7 +1411,10 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       b.kp_vis[o] = (b.kp_w[o] <= d) ? 2 : 1;
     }
   }
-  const uint32_t nl = min(b.n_labels, (uint32_t)kMaxLdsLabels);
+  // Label statistics (pixel count + tight box per label) only when the caller
+  // asked for them (csg_outputs.inst_stats): otherwise no LDS table, no runs.
+  const bool want_stats = b.stats != nullptr;
+  const uint32_t nl = want_stats ? min(b.n_labels, (uint32_t)kMaxLdsLabels) : 0u;
   uint32_t (*lstat)[kMaxLdsLabels] = L.q.lstat;
   for (uint32_t l = tid; l < nl; l += kBlock) {
     lstat[0][l] = 0; lstat[1][l] = 0xFFFFFFFFu; lstat[2][l] = 0xFFFFFFFFu; lstat[3][l] = 0; lstat[4][l] = 0;
@@ -1538,14 +1541,16 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
           n2 = e.n2;
           zrow[k] = (unsigned long long)rgb | ((unsigned long long)(uint32_t)id << 32);
           pend &= ~(1u << k);
-          if (id != run) {
-            flush_run();
-            run = id;
-            cnt = 0;
-            xmin = (uint32_t)px;
+          if (want_stats) {
+            if (id != run) {
+              flush_run();
+              run = id;
+              cnt = 0;
+              xmin = (uint32_t)px;
+            }
+            ++cnt;
+            xmax = (uint32_t)px;
           }
-          ++cnt;
-          xmax = (uint32_t)px;
         }
         if (b.depth) b.depth[qo + k] = dep;
         if (b.normals) {
