@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=384, help="frames rendered by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pcie-steps", type=int, default=3, help="batches timed with host outputs (0 = skip)")
+    ap.add_argument("--stats-steps", type=int, default=5, help="batches timed with label statistics (0 = skip)")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -156,6 +157,32 @@ def main():
     stage_ms = {k: tm[k] / K for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")}
     b_geom = wl.scene.authored_bytes()
 
+    # ---- with label statistics (rank 0, N=1 only; never `value`): the same
+    # batches also writing the per-label pixel count + tight 2D box that the
+    # generator's label records use (not part of the metric's outputs)
+    with_stats = None
+    if rank == 0 and world == 1 and args.stats_steps > 0:
+        try:
+            st_buf = torch.empty((F, r.n_labels, 5), dtype=torch.int32, device=dev)
+
+            def step_stats(k):
+                base = frames_dev.data_ptr() + (k % (W + K)) * F * fsz
+                r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), 0, kp_uv.data_ptr(), kp_vis.data_ptr(),
+                              stats=st_buf.data_ptr(), stream=stream)
+            step_stats(0)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for k in range(args.stats_steps):
+                step_stats(k)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t1
+            r.synchronize()
+            with_stats = {"value": round(args.stats_steps * F / dt, 2), "unit": "frames/s",
+                          "note": f"the timed batches plus per-label pixel count and 2D box (inst_stats); "
+                                  f"{args.stats_steps} batches of {F}"}
+        except Exception as e:  # the extra figure must never break the bench line
+            log(f"with-stats measurement failed: {e}")
+
     # ---- PCIe-inclusive rate (rank 0, N=1 only; never `value`): the same
     # batches with the outputs copied to pinned host buffers by the library
     pcie = None
@@ -222,6 +249,7 @@ def main():
                          "avg_launch_ms": round(raster_ms, 4), "valu": valu},
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "with_label_stats": with_stats,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "frame_roofline": {"B_frame": b_geom + b_tex + npx * 7,
                                "frac": round(value / world * (b_geom + b_tex + npx * 7) / (HBM_PEAK_GBS * 1e9), 5)},

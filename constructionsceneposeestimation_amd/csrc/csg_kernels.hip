@@ -1259,7 +1259,7 @@ struct ResolveLds {
   uint32_t keys[kShadeSlots];       // uid or kNoAlpha (empty)
   uint32_t more;                    // a pixel is left for another round
   ShadeEntry tab[kShadeSlots];
-  uint32_t lstat[5][kMaxLdsLabels]; // per-label pixel count + box
+  uint32_t lstat[3][kMaxLdsLabels]; // per label: pixel count, column mask, row mask (tile-relative bits)
 };
 
 // The resolve's LDS aliases the raster loop's in a union inside k_raster.
@@ -1417,7 +1417,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   const uint32_t nl = want_stats ? min(b.n_labels, (uint32_t)kMaxLdsLabels) : 0u;
   uint32_t (*lstat)[kMaxLdsLabels] = L.q.lstat;
   for (uint32_t l = tid; l < nl; l += kBlock) {
-    lstat[0][l] = 0; lstat[1][l] = 0xFFFFFFFFu; lstat[2][l] = 0xFFFFFFFFu; lstat[3][l] = 0; lstat[4][l] = 0;
+    lstat[0][l] = 0; lstat[1][l] = 0; lstat[2][l] = 0;
   }
   // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads.
   // Rounds: the tile's distinct winning triangles go into the shade table
@@ -1508,11 +1508,11 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       auto flush_run = [&]() {
         if (DBG(b.dbg) & 16384u) return;   // ablation only: no label stats
         if (run >= 0 && (uint32_t)run < nl) {
+          // the box as bit masks of the tile's columns and rows: 3 atomics per
+          // run instead of 5 (min/max are the lowest and highest bits)
           atomicAdd(&lstat[0][run], cnt);
-          atomicMin(&lstat[1][run], xmin);
-          atomicMin(&lstat[2][run], (uint32_t)qy);
-          atomicMax(&lstat[3][run], xmax);
-          atomicMax(&lstat[4][run], (uint32_t)qy);
+          atomicOr(&lstat[1][run], (0xFu >> (3u - (xmax - xmin))) << (xmin - (uint32_t)ox));
+          atomicOr(&lstat[2][run], 1u << ((uint32_t)qy - (uint32_t)oy));
         } else if (run >= 0 && b.stats && (uint32_t)run < b.n_labels) {   // beyond the LDS table
           uint32_t* st = b.stats + ((size_t)f * b.n_labels + (uint32_t)run) * 5;
           atomicAdd(&st[0], cnt);
@@ -1614,11 +1614,12 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     for (uint32_t l = tid; l < nl; l += kBlock) {
       const uint32_t cnt = lstat[0][l];
       if (cnt) {
+        const uint32_t cm = lstat[1][l], rm = lstat[2][l];
         atomicAdd(&st[l * 5 + 0], cnt);
-        atomicMin(&st[l * 5 + 1], lstat[1][l]);
-        atomicMin(&st[l * 5 + 2], lstat[2][l]);
-        atomicMax(&st[l * 5 + 3], lstat[3][l]);
-        atomicMax(&st[l * 5 + 4], lstat[4][l]);
+        atomicMin(&st[l * 5 + 1], (uint32_t)ox + (uint32_t)(__ffs(cm) - 1));
+        atomicMin(&st[l * 5 + 2], (uint32_t)oy + (uint32_t)(__ffs(rm) - 1));
+        atomicMax(&st[l * 5 + 3], (uint32_t)ox + 31u - (uint32_t)__clz(cm));
+        atomicMax(&st[l * 5 + 4], (uint32_t)oy + 31u - (uint32_t)__clz(rm));
       }
     }
   }

@@ -8,7 +8,7 @@ R=${ROUND:-r01}
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err &&
-(export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$R -o kt --output-format csv -- python3 bench.py --cpu-sample 0 > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err)
+(export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$R -o kt --output-format csv -- python3 bench.py --cpu-sample 0 --pcie-steps 0 --stats-steps 0 > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err)
 rc=$?
 echo "exit $rc"
 tail -3 gpurun_out/smoke.log; tail -3 gpurun_out/pytest_gpu.log; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err

@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=${ROUND:-r01}
-ARGS=${BENCH_ARGS:---steps 6 --warmup 1 --cpu-sample 0 --pcie-steps 0}
+ARGS=${BENCH_ARGS:---steps 6 --warmup 1 --cpu-sample 0 --pcie-steps 0 --stats-steps 0}
 OUT=gpurun_out/pmc_$R
 mkdir -p $OUT
 run() {  # name counters...
