@@ -1199,9 +1199,11 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
     cs = fabsf(d / len);
     // two-sided: the clip-space determinant is negative exactly when the face
     // normal points toward the camera (pixel projection with fx*fy > 0)
-    const float sg = facing ? 1.0f : -1.0f;
-    n01 = half_bits(sg * (nx / len)) | (half_bits(sg * (ny / len)) << 16);
-    n2 = half_bits(sg * (nz / len));
+    if (b.normals) {   // (three IEEE divisions: only when normals are an output)
+      const float sg = facing ? 1.0f : -1.0f;
+      n01 = half_bits(sg * (nx / len)) | (half_bits(sg * (ny / len)) << 16);
+      n2 = half_bits(sg * (nz / len));
+    }
   }
   e.n01 = n01;
   e.n2 = n2;
