@@ -1148,22 +1148,6 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   float p[9];
 #pragma unroll
   for (int z = 0; z < 9; ++z) p[z] = tp[z];
-  Cv3 v[3];
-  {
-    const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
-#pragma unroll
-    for (int z = 0; z < 3; ++z) {
-      v[z].x = dot4(Cm + 0, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
-      v[z].y = dot4(Cm + 4, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
-      v[z].w = dot4(Cm + 8, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
-    }
-  }
-  Hom h;
-  hom_setup(v, h);
-#pragma unroll
-  for (int z = 0; z < 3; ++z) { e.A[z] = h.A[z]; e.B[z] = h.B[z]; e.C[z] = h.C[z]; }
-  e.invdet = h.invdet;
-  const bool facing = h.invdet < 0.0f;
   e.label = m.label;
   const MatDesc mat = b.mats[(size_t)set * b.n_mat + m.material];
   const int tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
@@ -1172,6 +1156,26 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
 #pragma unroll
   for (int z = 0; z < 6; ++z) e.uv[z] = tex >= 0 ? tu[z] : 0.0f;
+  // Homogeneous coefficients: for texture coordinates, depth / points and the
+  // normals' facing sign only (a flat-shaded triangle without those outputs
+  // needs none of them: no clip transform, no IEEE reciprocal).
+  bool facing = false;
+  if (tex >= 0 || b.depth || b.points || b.normals) {
+    Cv3 v[3];
+    const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
+#pragma unroll
+    for (int z = 0; z < 3; ++z) {
+      v[z].x = dot4(Cm + 0, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
+      v[z].y = dot4(Cm + 4, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
+      v[z].w = dot4(Cm + 8, p[3 * z], p[3 * z + 1], p[3 * z + 2]);
+    }
+    Hom h;
+    hom_setup(v, h);
+#pragma unroll
+    for (int z = 0; z < 3; ++z) { e.A[z] = h.A[z]; e.B[z] = h.B[z]; e.C[z] = h.C[z]; }
+    e.invdet = h.invdet;
+    facing = h.invdet < 0.0f;
+  }
   // world-space edges e1 = pw1 - pw0, e2 = pw2 - pw0, one model row (= one
   // world coordinate) at a time
   float e1[3], e2[3];
