@@ -35,6 +35,9 @@ namespace csg {
 #define CSG_ABLATION 0         // 1: honour the CSG_DEBUG ablation / profiling bits (tools/ablate.sh builds)
 #endif
 #define DBG(d) (CSG_ABLATION ? (d) : 0u)
+#ifndef CSG_WRAP_FAST
+#define CSG_WRAP_FAST 1        // texel wrap: in-range coordinates skip the modulo (see wrap_index)
+#endif
 #ifndef CSG_TIGHT_ROWS
 #define CSG_TIGHT_ROWS 1       // staged row range widened by 1/16 px (not 1/2) for records near the tile
 #endif
@@ -119,6 +122,11 @@ struct TexTap { uint32_t i00, i10, i01, i11; int wx, wy; };
 // it; q*n and fu - q*n are integers below 2^24, so every step is exact.
 __device__ __forceinline__ int wrap_index(float fu, int n) {
   const float nf = (float)n;
+#if CSG_WRAP_FAST
+  // Texture coordinates inside one repeat (the usual case: uvs in [0, 1])
+  // need no reduction; the branch is skipped when no lane of the wave wraps.
+  if (fu >= 0.0f && fu < nf) return (int)fu;
+#endif
   const float q = floorf(fu * __builtin_amdgcn_rcpf(nf));
   float r = fu - q * nf;
   r += r < 0.0f ? nf : 0.0f;
