@@ -8,21 +8,24 @@
 // -ffp-contract=off on both sides; every float expression below is written
 // in the same order as there).
 //
-// Pipeline per batch of F frames (all frames of a batch in every launch):
-//   k_clip     (F x instances)   P*V*M in fp32, fixed summation order
-//   k_setup    (chunks x F)      chunk AABB cull, transform, triangle cull,
-//                                near-clip, fixed-point setup, wave-ballot
-//                                record append
-//   k_count    (64 x F)          LDS-aggregated per-tile record counts
+// Pipeline per launch chain of F frames (by default the whole batch):
+//   k_clip     (instances x F)   P*V*M in fp32, fixed summation order
+//   k_setup    (F x chunks)      chunk AABB cull, transform, triangle cull,
+//                                near-clip, fixed-point setup, exact cover
+//                                test of small records, wave-ballot append
+//   k_count    (128 x F)         LDS-aggregated per-tile record counts
 //   k_scan     (F)               exclusive scan of tile counts
-//   k_bin      (64 x F)          LDS-aggregated scatter of record ids to bins
-//   k_raster   (tiles x F)       32x32 tile: bins staged in LDS, balanced
-//                                (record,pixel) expansion, 64-bit
-//                                (depth,uid) z-buffer in LDS (ds_min_u64),
-//                                then resolve: texture, shade, instance id,
-//                                depth, coalesced HBM writes, label stats
+//   k_bin      (128 x F)         LDS-aggregated scatter of record ids to bins
 //   k_keypoints(K x F)           3D->2D keypoint projection (before k_raster;
 //                                k_raster depth-tests those in its tile)
+//   k_raster   (tiles x F)       32x32 tile: bins staged in LDS, (record,row)
+//                                then (span,pixel) expansion, 64-bit
+//                                (depth,uid) z-buffer in LDS (ds_min_u64),
+//                                then resolve: texture, shade, instance id,
+//                                optional depth / normals / points / label
+//                                stats, coalesced HBM writes
+// The kernels are VALU-issue bound: the code below trades
+// memory for instructions wherever the result is unchanged.
 #include <math.h>
 
 #include <type_traits>
