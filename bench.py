@@ -96,8 +96,16 @@ def main():
     frames_dev = torch.from_numpy(frames.view(np.uint8).copy()).to(dev)
     fsz = FRAME_DTYPE.itemsize
     Kp = r.n_kp
+    from constructionsceneposeestimation_amd.workload import WORKLOADS
+    outs = set(WORKLOADS[args.workload]["outputs"])   # C5 adds depth, normals and world points
     rgb = torch.empty((F, H, Wd, 3), dtype=torch.uint8, device=dev)
     inst = torch.empty((F, H, Wd), dtype=torch.int32, device=dev)
+    depth = torch.empty((F, H, Wd), dtype=torch.float32, device=dev) if "depth" in outs else None
+    normals = torch.empty((F, H, Wd, 3), dtype=torch.float16, device=dev) if "normals" in outs else None
+    points = torch.empty((F, H, Wd, 3), dtype=torch.float32, device=dev) if "points" in outs else None
+    extra = dict(depth=depth.data_ptr() if depth is not None else 0,
+                 normals=normals.data_ptr() if normals is not None else 0,
+                 points=points.data_ptr() if points is not None else 0)
     kp_uv = torch.empty((F, Kp, 2), dtype=torch.float32, device=dev)
     kp_vis = torch.empty((F, Kp), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -106,8 +114,8 @@ def main():
 
     def step(s):
         base = frames_dev.data_ptr() + s * F * fsz
-        r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), 0, kp_uv.data_ptr(), kp_vis.data_ptr(),
-                      stream=stream)
+        r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), kp_uv=kp_uv.data_ptr(), kp_vis=kp_vis.data_ptr(),
+                      stream=stream, **extra)
 
     for s in range(W):
         step(s)
@@ -134,7 +142,9 @@ def main():
 
     # ---- roofline of the dominant kernel (k_raster), HIP events on its stream
     npx = H * Wd
-    b_out = npx * (3 + 4)                                  # RGB8 + int32 instance per frame
+    px_bytes = 3 + 4 + (4 if depth is not None else 0) + (6 if normals is not None else 0) + \
+        (12 if points is not None else 0)                  # RGB8 + int32 instance (+ C5's f32 depth, f16x3, f32x3)
+    b_out = npx * px_bytes
     b_tex = int(wl.scene.texture_bytes())
     launches = max(tm["batches"], 1)                       # k_raster launches (one per launch chain)
     frames_per_launch = tm["frames"] / launches
@@ -167,8 +177,8 @@ def main():
 
             def step_stats(k):
                 base = frames_dev.data_ptr() + (k % (W + K)) * F * fsz
-                r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), 0, kp_uv.data_ptr(), kp_vis.data_ptr(),
-                              stats=st_buf.data_ptr(), stream=stream)
+                r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), kp_uv=kp_uv.data_ptr(),
+                              kp_vis=kp_vis.data_ptr(), stats=st_buf.data_ptr(), stream=stream, **extra)
             step_stats(0)
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
@@ -239,7 +249,8 @@ def main():
             "warmup": W, "ms_per_step": round(elapsed_max / K * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.workload}: world2.usd + crane/dumper/4 rigged-human proxies, "
-                                   f"{Wd}x{H}, RGB8 + int32 instance mask + {Kp} 2D keypoints/frame",
+                                   f"{Wd}x{H}, RGB8 + int32 instance mask + {Kp} 2D keypoints/frame"
+                                   + ("".join(f" + {o}" for o in ("depth", "normals", "points") if o in outs)),
                        "frames_per_step": F, "frames_per_launch": frames_per_launch, "seed": args.seed, "width": Wd, "height": H,
                        "tris_per_frame": wl.scene.n_tris_per_frame,
                        "parallelism": f"seed-sharded epochs x{world}, no collectives"},
@@ -251,8 +262,8 @@ def main():
             "pcie_inclusive": pcie,
             "with_label_stats": with_stats,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
-            "frame_roofline": {"B_frame": b_geom + b_tex + npx * 7,
-                               "frac": round(value / world * (b_geom + b_tex + npx * 7) / (HBM_PEAK_GBS * 1e9), 5)},
+            "frame_roofline": {"B_frame": b_geom + b_tex + npx * px_bytes,
+                               "frac": round(value / world * (b_geom + b_tex + npx * px_bytes) / (HBM_PEAK_GBS * 1e9), 5)},
             "records_per_frame": round(bst["records"] / max(bst["frames"], 1), 1),
             "bin_entries_per_frame": round(bst["bin_entries"] / max(bst["frames"], 1), 1),
         }
