@@ -335,3 +335,59 @@ def test_alpha_test_thresholds_and_shared_textures():
     seen = set(np.unique(ora["instance"]).tolist())
     assert {0, 1, 2, 3} <= seen, seen          # every card and the ground show through the cut-outs
     _assert_same(gpu, ora, 0)
+
+
+def test_random_triangle_soup_exact_coverage():
+    """Adversarial coverage: thousands of random triangles -- sub-pixel, slivers,
+    huge ones reaching far off-screen (the int64 row-span path), ones crossing
+    the near plane, many vertices snapped to pixel centres so edges run
+    exactly through centres (the top-left rule decides) -- bit-exact ids and
+    depth against the oracle (spans are computed from float boundaries and
+    walked only near centres)."""
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd.scene.model import Instance, Material, Mesh, Scene, SceneObject
+    rng = np.random.default_rng(11)
+    W, H = 320, 200
+    intr = cm.Intrinsics(W, H)
+    P = intr.pixel_projection()
+    C = np.eye(4)
+    V = cm.view_matrix(C)                      # camera at the origin looking along -Z
+
+    def unproject(u, v, d):                    # pixel (u, v) at distance d -> camera/world point
+        x = (u - W / 2) * d / intr.fx
+        y = -(v - H / 2) * d / intr.fy
+        return np.stack([x, y, -d], -1)
+
+    tris = []
+    n = 600
+    for kind in range(5):
+        u = rng.uniform(-20, W + 20, (n, 3))
+        v = rng.uniform(-20, H + 20, (n, 3))
+        d = rng.uniform(1.0, 40.0, (n, 1)) * np.ones((1, 3))
+        if kind == 0:                          # sub-pixel
+            u = u[:, :1] + rng.uniform(-0.8, 0.8, (n, 3)); v = v[:, :1] + rng.uniform(-0.8, 0.8, (n, 3))
+        elif kind == 1:                        # slivers
+            u[:, 2] = u[:, 0] + rng.uniform(-0.3, 0.3, n); v[:, 2] = v[:, 0] + rng.uniform(-0.3, 0.3, n)
+        elif kind == 2:                        # huge, far off-screen vertices
+            u[:, 1] = rng.uniform(-8000, 8000, n); v[:, 2] = rng.uniform(-8000, 8000, n)
+        elif kind == 3:                        # vertices on pixel centres
+            u = np.floor(u) + 0.5; v = np.floor(v) + 0.5
+        d += rng.uniform(-0.5, 0.5, (n, 3))
+        p = unproject(u, v, d)
+        if kind == 4:                          # crossing the near plane (0.5)
+            p[:, 0, 2] = rng.uniform(-0.45, 0.2, n)
+        tris.append(p)
+    pts = np.concatenate(tris).reshape(-1, 3).astype(np.float32)
+    idx = np.arange(pts.shape[0], dtype=np.uint32).reshape(-1, 3)
+    no_uv = (np.zeros((0, 2), np.float32), np.zeros((0, 3), np.uint32))
+    s = Scene()
+    s.materials = [Material("m", np.array([0.6, 0.5, 0.4]))]
+    half = idx.shape[0] // 2
+    s.meshes = [Mesh("a", pts, idx[:half].copy(), *no_uv, 0), Mesh("b", pts, idx[half:].copy(), *no_uv, 0)]
+    s.instances = [Instance(0, np.eye(4), 0, 0, np.eye(4)), Instance(1, np.eye(4), 1, 1, np.eye(4))]
+    s.objects = [SceneObject(f"/r{k}", "fence", 2, k) for k in range(2)]
+    ora = _oracle(s, W, H).render(V, P)
+    with _renderer(s, W, H, 1) as r:
+        gpu = r.render(_frames(V[None], P[None]))
+    assert (ora["instance"] >= 0).mean() > 0.3
+    _assert_same(gpu, ora, 0)
