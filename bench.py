@@ -10,21 +10,35 @@ segmentation + 2D keypoints) rendered into HBM-resident output buffers.
 Frames are seed-sharded: rank r owns randomisation epochs e = r (mod N),
 10 frames per epoch, so per-GPU work is fixed as N grows ("weak" scaling)
 and no collective touches the data path; the only inter-rank traffic is the
-gloo barrier and the max-over-ranks of the elapsed time.
+gloo barrier, the max-over-ranks of the elapsed time and the verification
+counts.
 
-Inputs (camera/instance/keypoint parameters of every frame of every step)
-are uploaded to HBM before the timed region.  Reported extras:
-``roofline`` for the dominant kernel (k_raster) timed with HIP events on its
-launch stream, and ``cpu_baseline`` = the CPU oracle (a port of the same
-arithmetic; the reference has no CPU render path) on a bounded sample.
+The line validates what it timed before it prints a number:
+* the library's overflow word is sticky across asynchronous batches, so the
+  ``synchronize()`` after the timed loop fails if any warm-up or timed batch
+  truncated its records or bin lists (no line is printed);
+* frames of the last timed step are rendered again by the CPU oracle and
+  compared byte for byte with what the GPU wrote during the timed region
+  (RGB, instance ids, keypoint uv bits and visibility); any difference
+  aborts the run.  On rank 0 at N=1 the same oracle runs are the CPU
+  baseline.
+
+Reported extras: ``roofline`` (B_frame x frames per launch /
+the average k_raster launch timed with HIP events on its stream, plus per-
+kernel entries and the frame-level fraction fps x B_frame / peak) and
+``cpu_baseline`` (oracle/csg_oracle.c, a port of the same arithmetic -- the
+reference has no CPU render path -- single-thread and all-cores, median of 5
+after a warm-up, wall clock without file I/O).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 
@@ -33,23 +47,198 @@ sys.path.insert(0, ROOT)
 
 METRIC = "annotated frames/sec (RGB+seg+2D kpts) at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+RECORD_BYTES = 112 + 4  # k_setup writes one 112-B raster record + its 4-B tile rectangle per record
+DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 240
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ---------------------------------------------------------------------------
+# host arithmetic (unit-tested on CPU: tests/test_bench_logic.py)
+# ---------------------------------------------------------------------------
+
+def rank_frames(rank: int, world: int, steps: int, frames_per_step: int) -> List[int]:
+    """Frame ids of every step of ``rank``: the epoch-interleaved seed shard
+    (SURVEY §8e), ``steps * frames_per_step`` frames, step s = slice s."""
+    from constructionsceneposeestimation_amd.shard import shard_frames
+    return shard_frames(rank, world, steps * frames_per_step)
+
+
+def timed_frames(fids: List[int], warmup: int, steps: int, frames_per_step: int) -> List[int]:
+    return fids[warmup * frames_per_step:(warmup + steps) * frames_per_step]
+
+
+def verify_sample_indices(frames_per_step: int, n: int) -> List[int]:
+    """``n`` distinct frame slots of one step, evenly spread, first and last included."""
+    n = max(0, min(n, frames_per_step))
+    if n == 0:
+        return []
+    if n == 1:
+        return [frames_per_step - 1]
+    return [int(round(k * (frames_per_step - 1) / (n - 1))) for k in range(n)]
+
+
+def aggregate_value(steps: int, frames_per_step: int, world: int, elapsed_max: float) -> float:
+    """Whole-job frames/s: every rank renders ``steps * frames_per_step`` frames."""
+    return steps * frames_per_step * world / elapsed_max
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world <= 1:
+        return float(x)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(vals: List[int], world: int) -> List[int]:
+    if world <= 1:
+        return [int(v) for v in vals]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(v) for v in vals], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(v) for v in t.tolist()]
+
+
+def median_time(fn: Callable[[], None], runs: int = 5, warmup: int = 1) -> float:
+    """Median wall time of ``runs`` calls after ``warmup`` untimed ones."""
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
+def roofline(b_geom: int, b_tex: int, b_out: int, frames_per_launch: float, raster_ms: float, setup_ms: float,
+             records_per_frame: float, fps: float, traffic: Optional[Dict[str, int]] = None) -> dict:
+    """B_frame = B_geom + B_tex + B_out per frame.  The headline
+    entry prices B_frame x frames per launch against the dominant kernel's
+    (k_raster) average launch; per-kernel entries price each kernel's own
+    algorithmic bytes; ``frame_level`` is fps x B_frame / peak."""
+    traffic = traffic or {}
+    b_frame = b_geom + b_tex + b_out
+    bpl = int(round(frames_per_launch * b_frame))
+    achieved = bpl / (raster_ms * 1e-3) / 1e9
+
+    def kern(name, nbytes, ms, what):
+        a = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        return {"kernel": name, "bytes_per_launch": int(nbytes), "avg_launch_ms": round(ms, 4),
+                "achieved": round(a, 2), "frac": round(a / HBM_PEAK_GBS, 5), "traffic": traffic.get(name),
+                "bytes": what}
+
+    kernels = [
+        kern("k_raster", round(frames_per_launch * (b_tex + b_out)), raster_ms,
+             "B_out + B_tex: outputs written once, bound textures read once"),
+        kern("k_setup", round(frames_per_launch * (b_geom + records_per_frame * RECORD_BYTES)), setup_ms,
+             "B_geom + raster records: authored geometry read once, 116 B written per record (k_clip + k_setup)"),
+    ]
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic.get("k_raster"), "kernel": "k_raster",
+            "bytes_per_launch": bpl, "avg_launch_ms": round(raster_ms, 4),
+            "formula": "B_frame (SURVEY §8(d)) x frames per launch / k_raster average launch (HIP events on its stream)",
+            "kernels": kernels,
+            "frame_level": {"B_frame": int(b_frame), "B_geom": int(b_geom), "B_tex": int(b_tex), "B_out": int(b_out),
+                            "frac": round(fps * b_frame / (HBM_PEAK_GBS * 1e9), 5)}}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def available_cpus() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+# ---------------------------------------------------------------------------
+# oracle check of the timed outputs (checker only: tests/, smoke() and this leg)
+# ---------------------------------------------------------------------------
+
+class Verifier:
+    """Renders sampled frames with the CPU oracle and compares them with the
+    GPU's outputs of the same frames."""
+
+    def __init__(self, wl, want_kp: bool):
+        from constructionsceneposeestimation_amd.packing import pack_scene
+        from oracle.oracle import Oracle
+        self.wl, self.want_kp = wl, want_kp
+        self.o = Oracle(pack_scene(wl.scene), wl.width, wl.height)
+        self.extra = any(k in wl.outputs for k in ("normals", "points"))
+
+    def render(self, frames: List[int], threads: int):
+        """(rgb, inst, depth[, normals, points]) of ``frames``; frames of DR
+        epochs (C4) or with C5 outputs are rendered one by one."""
+        wl, o = self.wl, self.o
+        v, p = wl.frame_params(frames)
+        if not wl.dr and not self.extra:
+            models = np.stack([wl.epoch(f // 10).models.reshape(-1, 16) for f in frames])
+            rgb, inst, depth = o.render_many(v, p, threads=threads, outputs=True, models=models)
+            return v, p, {"rgb": rgb, "instance": inst, "depth": depth}
+        outs = {}
+        for k, f in enumerate(frames):
+            st = wl.epoch(f // 10)
+            o.set_instance_models(st.models.reshape(-1, 16))
+            if st.dr is not None:
+                o.set_light(st.dr.light)
+                o.set_material_textures(st.dr.textures)
+            r = o.render(v[k], p[k], extra=self.extra)
+            for key, a in r.items():
+                if key != "inst_stats":
+                    outs.setdefault(key, []).append(a)
+        return v, p, {k: np.stack(a) for k, a in outs.items()}
+
+    def compare(self, frames: List[int], v, p, ref: Dict[str, np.ndarray], gpu: Dict[str, np.ndarray]) -> List[str]:
+        bad = []
+        for k, f in enumerate(frames):
+            for key, g in gpu.items():
+                if key.startswith("keypoints") or key not in ref:
+                    continue
+                a, b = g[k], ref[key][k]
+                if a.dtype.kind == "f":
+                    a, b = a.view(np.uint32 if a.itemsize == 4 else np.uint16), b.view(np.uint32 if b.itemsize == 4 else np.uint16)
+                if not np.array_equal(a, b):
+                    bad.append(f"frame {f}: {key} ({int((a != b).sum())} values differ)")
+            if self.want_kp:
+                uv, vis = self.o.keypoints(v[k], p[k], self.wl.epoch(f // 10).keypoints, ref["depth"][k])
+                if not np.array_equal(gpu["keypoints_uv"][k].view(np.uint32), uv.view(np.uint32)):
+                    bad.append(f"frame {f}: keypoint uv")
+                if not np.array_equal(gpu["keypoints_vis"][k], vis):
+                    bad.append(f"frame {f}: keypoint visibility")
+        return bad
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames-per-step", type=int, default=240)
+    ap.add_argument("--steps", type=int, default=DEFAULT_STEPS)
+    ap.add_argument("--warmup", type=int, default=DEFAULT_WARMUP)
+    ap.add_argument("--frames-per-step", type=int, default=DEFAULT_FRAMES_PER_STEP)
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--frames-per-launch", type=int, default=0, help="frames per kernel chain (0 = library default)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=384, help="frames rendered by the CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--verify-frames", type=int, default=32,
+                    help="frames of the last timed step re-rendered by the oracle and compared (rank 0 at N=1: "
+                         "also the all-cores CPU baseline sample); 0 skips the check and the CPU baseline")
+    ap.add_argument("--verify-frames-multi", type=int, default=4, help="frames each rank checks when N > 1")
+    ap.add_argument("--cpu-single-frames", type=int, default=3, help="frames of the single-thread CPU baseline run")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU run (0 = all available)")
     ap.add_argument("--pcie-steps", type=int, default=3, help="batches timed with host outputs (0 = skip)")
     ap.add_argument("--stats-steps", type=int, default=5, help="batches timed with label statistics (0 = skip)")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -67,8 +256,7 @@ def main():
         dist.init_process_group("gloo", init_method="env://")
 
     from constructionsceneposeestimation_amd.renderer import FRAME_DTYPE, Renderer, make_frames
-    from constructionsceneposeestimation_amd.shard import shard_frames
-    from constructionsceneposeestimation_amd.workload import Workload
+    from constructionsceneposeestimation_amd.workload import WORKLOADS, Workload
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -76,18 +264,20 @@ def main():
     K, W = args.steps, args.warmup
     wl = Workload(args.workload, seed=args.seed)
     H, Wd = wl.height, wl.width
+    outs = set(WORKLOADS[args.workload]["outputs"])   # C5 adds depth, normals and world points
+    want_kp = "keypoints" in outs
     t0 = time.time()
 
     # ---- schedule for every step, uploaded before timing -------------------
-    total = (W + K) * F
-    fids = shard_frames(rank, world, total)
+    fids = rank_frames(rank, world, W + K, F)
     epochs = sorted({f // 10 for f in fids})
     set_of = {e: i for i, e in enumerate(epochs)}
     r = Renderer(wl.scene, Wd, H, max_frames=F, device=local, frames_per_launch=args.frames_per_launch)
     for e in epochs:
         st = wl.epoch(e)
         r.set_instance_transforms(set_of[e], st.models)
-        r.set_keypoints(set_of[e], st.keypoints)
+        if want_kp:
+            r.set_keypoints(set_of[e], st.keypoints)
         if st.dr is not None:                      # C4: per-epoch lighting and texture DR
             r.set_dr_light(set_of[e], st.dr.light)
             r.set_dr_textures(set_of[e], st.dr.textures)
@@ -96,31 +286,32 @@ def main():
     frames_dev = torch.from_numpy(frames.view(np.uint8).copy()).to(dev)
     fsz = FRAME_DTYPE.itemsize
     Kp = r.n_kp
-    from constructionsceneposeestimation_amd.workload import WORKLOADS
-    outs = set(WORKLOADS[args.workload]["outputs"])   # C5 adds depth, normals and world points
     rgb = torch.empty((F, H, Wd, 3), dtype=torch.uint8, device=dev)
     inst = torch.empty((F, H, Wd), dtype=torch.int32, device=dev)
-    depth = torch.empty((F, H, Wd), dtype=torch.float32, device=dev) if "depth" in outs else None
-    normals = torch.empty((F, H, Wd, 3), dtype=torch.float16, device=dev) if "normals" in outs else None
-    points = torch.empty((F, H, Wd, 3), dtype=torch.float32, device=dev) if "points" in outs else None
-    extra = dict(depth=depth.data_ptr() if depth is not None else 0,
-                 normals=normals.data_ptr() if normals is not None else 0,
-                 points=points.data_ptr() if points is not None else 0)
-    kp_uv = torch.empty((F, Kp, 2), dtype=torch.float32, device=dev)
-    kp_vis = torch.empty((F, Kp), dtype=torch.int32, device=dev)
+    dev_out = {"rgb": rgb, "instance": inst}
+    if "depth" in outs:
+        dev_out["depth"] = torch.empty((F, H, Wd), dtype=torch.float32, device=dev)
+    if "normals" in outs:
+        dev_out["normals"] = torch.empty((F, H, Wd, 3), dtype=torch.float16, device=dev)
+    if "points" in outs:
+        dev_out["points"] = torch.empty((F, H, Wd, 3), dtype=torch.float32, device=dev)
+    extra = {k: dev_out[k].data_ptr() for k in ("depth", "normals", "points") if k in dev_out}
+    if want_kp:
+        dev_out["keypoints_uv"] = torch.empty((F, Kp, 2), dtype=torch.float32, device=dev)
+        dev_out["keypoints_vis"] = torch.empty((F, Kp), dtype=torch.int32, device=dev)
+        extra.update(kp_uv=dev_out["keypoints_uv"].data_ptr(), kp_vis=dev_out["keypoints_vis"].data_ptr())
     stream = torch.cuda.current_stream(dev).cuda_stream
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s: {len(fids)} frames, {len(epochs)} epochs, "
         f"{wl.scene.n_tris_per_frame} tris/frame, K={Kp} keypoints")
 
-    def step(s):
+    def step(s, **kw):
         base = frames_dev.data_ptr() + s * F * fsz
-        r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), kp_uv=kp_uv.data_ptr(), kp_vis=kp_vis.data_ptr(),
-                      stream=stream, **extra)
+        r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), stream=stream, **extra, **kw)
 
     for s in range(W):
         step(s)
     torch.cuda.synchronize(dev)
-    r.synchronize()           # surfaces work-buffer overflow before timing
+    r.synchronize()           # raises on any warm-up overflow (sticky flag), then clears it
     r.timing_reset()
     if world > 1:
         dist.barrier()
@@ -132,58 +323,101 @@ def main():
     elapsed = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
+    # The overflow flag is sticky across the asynchronous batches: this raises
+    # (and no line is printed) if any timed batch truncated records or bins.
     r.synchronize()
     tm = r.timing_read()
     bst = r.batch_stats()
-    el = torch.tensor([elapsed], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed_max = float(el.item())
+    elapsed_max = max_over_ranks(elapsed, world)
 
-    # ---- roofline of the dominant kernel (k_raster), HIP events on its stream
+    # ---- the last timed step's outputs, copied before anything reuses them --
+    nver = args.verify_frames if world == 1 else min(args.verify_frames, args.verify_frames_multi)
+    vidx = verify_sample_indices(F, nver)
+    last = fids[(W + K - 1) * F:(W + K) * F]
+    sample_frames = [last[k] for k in vidx]
+    gpu_sample = {}
+    if vidx:
+        ix = torch.tensor(vidx, device=dev)
+        gpu_sample = {k: t.index_select(0, ix).cpu().numpy() for k, t in dev_out.items()}
+
+    # ---- roofline (HIP events on the launch stream) --------------------------
     npx = H * Wd
-    px_bytes = 3 + 4 + (4 if depth is not None else 0) + (6 if normals is not None else 0) + \
-        (12 if points is not None else 0)                  # RGB8 + int32 instance (+ C5's f32 depth, f16x3, f32x3)
+    px_bytes = 3 + 4 + (4 if "depth" in dev_out else 0) + (6 if "normals" in dev_out else 0) + \
+        (12 if "points" in dev_out else 0)             # RGB8 + int32 instance (+ C5's f32 depth, f16x3, f32x3)
     b_out = npx * px_bytes
     b_tex = int(wl.scene.texture_bytes())
-    launches = max(tm["batches"], 1)                       # k_raster launches (one per launch chain)
+    b_geom = int(wl.scene.authored_bytes())
+    launches = max(tm["batches"], 1)                   # k_raster launches (one per launch chain)
     frames_per_launch = tm["frames"] / launches
-    bytes_per_launch = int(round(frames_per_launch * (b_out + b_tex)))
-    raster_ms = tm["ms_raster"] / launches
-    achieved = bytes_per_launch / (raster_ms * 1e-3) / 1e9
-    traffic = valu = None
+    value = aggregate_value(K, F, world, elapsed_max)
+    traffic = None
+    valu = None
     if os.path.exists(args.profile_json):
         try:
             pj = json.load(open(args.profile_json))
-            if pj.get("workload") == args.workload and pj.get("frames_per_launch") == frames_per_launch:
-                traffic = pj.get("k_raster_bytes_per_launch")
+            if (pj.get("workload") == args.workload and pj.get("frames_per_launch") == frames_per_launch
+                    and pj.get("B_frame") == b_geom + b_tex + b_out):
+                traffic = {k: v for k, v in pj.get("bytes_per_launch", {}).items()}
                 if pj.get("k_raster_valu_busy") is not None:
                     valu = {"busy": round(pj["k_raster_valu_busy"], 3),
                             "lane_util": round(pj.get("k_raster_valu_lane_util") or 0.0, 3),
-                            "note": "the kernel's actual limiter: VALU issue (rocprofv3 SQ_ACTIVE_INST_VALU, "
+                            "note": "k_raster's limiter: VALU issue (rocprofv3 SQ_ACTIVE_INST_VALU, "
                                     "profiles/pmc_traffic.json)"}
         except Exception:
             traffic = valu = None
-    stage_ms = {k: tm[k] / K for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")}
-    b_geom = wl.scene.authored_bytes()
+    rf = roofline(b_geom, b_tex, b_out, frames_per_launch, tm["ms_raster"] / launches, tm["ms_setup"] / launches,
+                  bst["records"] / max(bst["frames"], 1), value / world, traffic)
+    rf["valu"] = valu
+    if traffic is not None:
+        rf["traffic_note"] = ("HBM bytes per launch from rocprofv3 PMC: FETCH_SIZE x 2 (gfx950 counts half of a "
+                              "128-B read request, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, KB = 1024 B")
 
-    # ---- with label statistics (rank 0, N=1 only; never `value`): the same
-    # batches also writing the per-label pixel count + tight 2D box that the
-    # generator's label records use (not part of the metric's outputs)
+    # ---- verification + CPU baseline (oracle) --------------------------------
+    cpu = None
+    bad: List[str] = []
+    if vidx:
+        ver = Verifier(wl, want_kp)
+        if rank == 0 and world == 1:
+            # the box's CPU share (OMP_NUM_THREADS is set to it there), else every CPU of this process
+            thr = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or available_cpus()
+            res = {}
+
+            def run_all():
+                res["out"] = ver.render(sample_frames, thr)
+            t_all = median_time(run_all, runs=5, warmup=1)
+            n1 = max(1, min(args.cpu_single_frames, len(sample_frames)))
+            t_one = median_time(lambda: ver.render(sample_frames[:n1], 1), runs=5, warmup=1)
+            v_, p_, ref = res["out"]
+            bad = ver.compare(sample_frames, v_, p_, ref, gpu_sample)
+            cpu = {"value": round(len(sample_frames) / t_all, 3), "unit": "frames/s", "cores": thr, "kind": "port",
+                   "single_thread": round(n1 / t_one, 3),
+                   "sample": f"{len(sample_frames)} frames of the last timed step of the {args.workload} schedule "
+                             f"(seed {args.seed}) at {Wd}x{H} with {thr} OpenMP threads, {n1} of them single-threaded; "
+                             f"oracle/csg_oracle.c, median of 5 after 1 warm-up, wall clock, no file I/O",
+                   "method": "median of 5 after 1 warm-up", "nproc": os.cpu_count(), "available_cpus": available_cpus(),
+                   "cpu_model": cpu_model()}
+        else:
+            v_, p_, ref = ver.render(sample_frames, 2)
+            bad = ver.compare(sample_frames, v_, p_, ref, gpu_sample)
+    n_checked, n_bad = sum_over_ranks([len(sample_frames), len(bad)], world)
+    if n_bad:
+        for b in bad[:20]:
+            log(f"[rank {rank}] VERIFY FAILED: {b}")
+        log(f"[rank {rank}] {n_bad} mismatches between the timed GPU outputs and the oracle: no result")
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(3)
+
+    # ---- with label statistics (rank 0, N=1 only; never `value`) -------------
     with_stats = None
     if rank == 0 and world == 1 and args.stats_steps > 0:
         try:
             st_buf = torch.empty((F, r.n_labels, 5), dtype=torch.int32, device=dev)
-
-            def step_stats(k):
-                base = frames_dev.data_ptr() + (k % (W + K)) * F * fsz
-                r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), kp_uv=kp_uv.data_ptr(),
-                              kp_vis=kp_vis.data_ptr(), stats=st_buf.data_ptr(), stream=stream, **extra)
-            step_stats(0)
+            step(0, stats=st_buf.data_ptr())
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
             for k in range(args.stats_steps):
-                step_stats(k)
+                step(k % (W + K), stats=st_buf.data_ptr())
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t1
             r.synchronize()
@@ -193,8 +427,7 @@ def main():
         except Exception as e:  # the extra figure must never break the bench line
             log(f"with-stats measurement failed: {e}")
 
-    # ---- PCIe-inclusive rate (rank 0, N=1 only; never `value`): the same
-    # batches with the outputs copied to pinned host buffers by the library
+    # ---- PCIe-inclusive rate (rank 0, N=1 only; never `value`) ---------------
     pcie = None
     if rank == 0 and world == 1 and args.pcie_steps > 0:
         try:
@@ -202,10 +435,10 @@ def main():
             from constructionsceneposeestimation_amd import _lib
             h_rgb = torch.empty((F, H, Wd, 3), dtype=torch.uint8, pin_memory=True)
             h_inst = torch.empty((F, H, Wd), dtype=torch.int32, pin_memory=True)
-            h_uv = torch.empty((F, Kp, 2), dtype=torch.float32, pin_memory=True)
-            h_vis = torch.empty((F, Kp), dtype=torch.int32, pin_memory=True)
-            o = _lib.Outputs(h_rgb.data_ptr(), h_inst.data_ptr(), None, h_uv.data_ptr(), h_vis.data_ptr(), None,
-                             r.n_labels, 0, None, None)
+            h_uv = torch.empty((F, max(Kp, 1), 2), dtype=torch.float32, pin_memory=True)
+            h_vis = torch.empty((F, max(Kp, 1)), dtype=torch.int32, pin_memory=True)
+            o = _lib.Outputs(h_rgb.data_ptr(), h_inst.data_ptr(), None, h_uv.data_ptr() if want_kp else None,
+                             h_vis.data_ptr() if want_kp else None, None, r.n_labels, 0, None, None)
             hframes = np.ascontiguousarray(frames[:F])
             r._check(r.lib.csg_render_batch_async(r.ctx, hframes.ctypes.data, F, 0, C.byref(o), None), "pcie")
             r.synchronize()
@@ -220,50 +453,27 @@ def main():
         except Exception as e:  # the extra figure must never break the bench line
             log(f"pcie-inclusive measurement failed: {e}")
 
-    # ---- CPU baseline (rank 0, N=1 only): the oracle on a bounded sample ----
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        try:
-            from constructionsceneposeestimation_amd.packing import pack_scene
-            from oracle.oracle import Oracle
-            ncpu = os.cpu_count() or 1
-            thr = max(1, min(args.cpu_threads, ncpu))
-            sample = fids[:args.cpu_sample]
-            o = Oracle(pack_scene(wl.scene), Wd, H)
-            v, p = wl.frame_params(sample)
-            models = np.stack([wl.epoch(f // 10).models.reshape(-1, 16) for f in sample])
-            t1 = time.perf_counter()
-            o.render_many(v, p, threads=thr, outputs=True, models=models)
-            n_done = len(sample)
-            cpu_t = time.perf_counter() - t1
-            cpu = {"value": round(n_done / cpu_t, 3), "unit": "frames/s", "cores": thr, "kind": "port",
-                   "sample": f"{n_done} frames of the timed {args.workload} schedule (seed {args.seed}) at "
-                             f"{Wd}x{H}, oracle/csg_oracle.c with {thr} OpenMP threads, {cpu_t:.1f}s wall"}
-        except Exception as e:  # the baseline must never break the bench line
-            log(f"cpu baseline failed: {e}")
-
     if rank == 0:
-        value = K * F * world / elapsed_max
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": K,
             "warmup": W, "ms_per_step": round(elapsed_max / K * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{args.workload}: world2.usd + crane/dumper/4 rigged-human proxies, "
-                                   f"{Wd}x{H}, RGB8 + int32 instance mask + {Kp} 2D keypoints/frame"
-                                   + ("".join(f" + {o}" for o in ("depth", "normals", "points") if o in outs)),
-                       "frames_per_step": F, "frames_per_launch": frames_per_launch, "seed": args.seed, "width": Wd, "height": H,
-                       "tris_per_frame": wl.scene.n_tris_per_frame,
+            "config": {"workload": f"{args.workload}: " + WORKLOADS[args.workload]["title"]
+                                   + f", {Wd}x{H}, RGB8 + int32 instance mask"
+                                   + (f" + {Kp} 2D keypoints/frame" if want_kp else "")
+                                   + "".join(f" + {o}" for o in ("depth", "normals", "points") if o in outs),
+                       "frames_per_step": F, "frames_per_launch": frames_per_launch, "seed": args.seed,
+                       "width": Wd, "height": H, "tris_per_frame": wl.scene.n_tris_per_frame,
                        "parallelism": f"seed-sharded epochs x{world}, no collectives"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "k_raster", "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": round(raster_ms, 4), "valu": valu},
+            "roofline": rf,
             "cpu_baseline": cpu,
+            "verified": {"frames": n_checked, "bit_exact": n_checked > 0,
+                         "outputs": sorted(gpu_sample) if gpu_sample else [],
+                         "against": "oracle/csg_oracle.c on frames of the last timed step",
+                         "overflow": "none: sticky flag checked after the warm-up and after the timed steps"},
             "pcie_inclusive": pcie,
             "with_label_stats": with_stats,
-            "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
-            "frame_roofline": {"B_frame": b_geom + b_tex + npx * px_bytes,
-                               "frac": round(value / world * (b_geom + b_tex + npx * px_bytes) / (HBM_PEAK_GBS * 1e9), 5)},
+            "stage_ms_per_step": {k: round(tm[k] / K, 4) for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")},
             "records_per_frame": round(bst["records"] / max(bst["frames"], 1), 1),
             "bin_entries_per_frame": round(bst["bin_entries"] / max(bst["frames"], 1), 1),
         }

@@ -12,7 +12,7 @@ from typing import Optional
 PKG = os.path.dirname(os.path.abspath(__file__))
 # CSG_LIB names an alternative build of the same ABI (A/B timing of kernel variants)
 LIB_PATH = os.environ.get("CSG_LIB") or os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 5  # CSG_ABI_VERSION in include/csg_api.h
+ABI_VERSION = 6  # CSG_ABI_VERSION in include/csg_api.h
 KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
 
 EXPORTED = (

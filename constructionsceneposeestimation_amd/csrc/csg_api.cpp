@@ -107,7 +107,20 @@ struct csg_ctx {
   // per-batch work buffers
   uint32_t rec_cap = 0, bin_cap = 0, work_frames = 0;
   DevBuf<FrameDev> frames;
-  FrameDev* h_frames = nullptr;         // pinned staging
+  // Pinned staging ring for host frame records: a batch's records are copied
+  // into the next slot, and a slot is reused only after the H2D copy that read
+  // it has completed (its event), so back-to-back async batches never render
+  // each other's cameras.
+  static constexpr uint32_t kStaging = 4;
+  FrameDev* h_stage[kStaging] = {};
+  hipEvent_t stage_ev[kStaging] = {};
+  bool stage_busy[kStaging] = {};
+  uint32_t stage_next = 0;
+  // The stream of the most recent enqueue.  The work buffers are shared, so a
+  // batch on a different stream first waits for the previous stream to drain;
+  // csg_synchronize waits on it.
+  hipStream_t last_stream = nullptr;
+  DevBuf<uint32_t> fset;                // [chain frames] checked transform set of each frame (k_clip)
   DevBuf<float> clip, pv;
   DevBuf<Rec> recs;
   DevBuf<uint32_t> rect, rec_count, tile_count, tile_off, tile_fill, bins, overflow;
@@ -151,6 +164,38 @@ struct csg_ctx {
                          hipGetErrorString(_e));                                                     \
   } while (0)
 
+// Wait for everything this context enqueued, on its own stream and on the
+// caller's stream of the most recent batch.
+static int drain(csg_ctx* c) {
+  if (c->last_stream && c->last_stream != c->stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+  if (c->stream) HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return CSG_OK;
+}
+
+// Read the sticky overflow / error word of every batch since it was last
+// read, clear it, and turn it into a status.  Callers have drained the streams.
+static int take_flags(csg_ctx* c, uint32_t* flags_out) {
+  uint32_t ov = 0;
+  HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
+  if ((c->dbg & 512u)) {   // profiling counters, cumulative since the context was created
+    uint32_t ctr[16];
+    HIP_TRY(c, hipMemcpy(ctr, c->overflow.p, sizeof(ctr), hipMemcpyDeviceToHost));
+    fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u alpha_fail %u alpha_pass %u early_z %u "
+            "wide_rows %u culled_recs %u culled_rows %u mask_rows %u\n", ctr[1], ctr[2], ctr[3], ctr[4], ctr[5],
+            ctr[6], ctr[7], ctr[8], ctr[9], ctr[10], ctr[11]);
+  }
+  if (flags_out) *flags_out = ov;
+  if (!ov) return CSG_OK;
+  HIP_TRY(c, hipMemset(c->overflow.p, 0, 4));
+  if (ov & (kOvBadSet | kOvBadKpSet))
+    return c->fail(CSG_ERR_INVALID,
+                   "device frame records named a transform set >= %u or a keypoint set >= %u (flags %u); those "
+                   "frames rendered with set 0 / without keypoints",
+                   (unsigned)c->set_valid.size(), (unsigned)c->kp_valid.size(), ov);
+  return c->fail(CSG_ERR_OVERFLOW, "work buffer overflow (flags %u): records_per_frame=%u bins_per_frame=%u", ov,
+                 c->rec_cap, c->bin_cap);
+}
+
 extern "C" {
 
 int csg_abi_version(void) { return CSG_ABI_VERSION; }
@@ -178,6 +223,13 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   c->ring.assign((size_t)csg_ctx::kRing * 5, nullptr);
   c->ring_frames.assign(csg_ctx::kRing, 0);
   for (size_t k = 0; k < c->ring.size() && e == hipSuccess; ++k) e = hipEventCreate(&c->ring[k]);
+  for (uint32_t k = 0; k < csg_ctx::kStaging && e == hipSuccess; ++k)
+    e = hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming);
+  // the overflow / error word lives as long as the context: it is sticky across
+  // asynchronous batches and cleared only when csg_synchronize or
+  // csg_render_batch has read it
+  if (e == hipSuccess) e = c->overflow.alloc(16);
+  if (e == hipSuccess) e = hipMemset(c->overflow.p, 0, 16 * sizeof(uint32_t));
   c->ev = c->ring.data();
   if (e != hipSuccess) {
     c->err = hipGetErrorString(e);
@@ -190,6 +242,7 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
 
 void csg_destroy(csg_ctx* c) {
   if (!c) return;
+  if (c->last_stream && c->last_stream != c->stream) (void)hipStreamSynchronize(c->last_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->set_mats.release(); c->lights.release();
   c->chunks.release();
@@ -201,8 +254,11 @@ void csg_destroy(csg_ctx* c) {
   c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
   c->kp_w.release(); c->kp_pix.release(); c->kp_tiles.release();
-  c->o_points.release(); c->o_normals.release(); c->cam.release();
-  if (c->h_frames) (void)hipHostFree(c->h_frames);
+  c->o_points.release(); c->o_normals.release(); c->cam.release(); c->fset.release();
+  for (uint32_t k = 0; k < csg_ctx::kStaging; ++k) {
+    if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
+    if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);
+  }
   for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -216,6 +272,10 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
     return c->fail(CSG_ERR_INVALID, "upload_scene: empty scene");
   if (n_inst >= kMaxInstances) return c->fail(CSG_ERR_LIMIT, "upload_scene: %u instances >= %u", n_inst, kMaxInstances);
   HIP_TRY(c, hipSetDevice(c->cfg.device));
+  {  // batches in flight read the scene and the work buffers this replaces
+    const int rc = drain(c);
+    if (rc) return rc;
+  }
   std::vector<float> pos, uvs;
   std::vector<uint32_t> tris, uvt;
   std::vector<MeshDesc> md(n_meshes);
@@ -318,7 +378,9 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   c->n_kp = 0;
   c->kp_dirty = true;
   c->have_scene = true;
-  c->work_frames = 0;  // re-size work buffers
+  c->work_frames = 0;  // re-size work buffers,
+  c->rec_cap = 0;      // with caps derived from this scene (or the config's fixed ones)
+  c->bin_cap = 0;
   return CSG_OK;
 }
 
@@ -455,6 +517,12 @@ static int build_alpha_classes(csg_ctx* c, const std::vector<TexDesc>& td, size_
 
 static int sync_scene_state(csg_ctx* c) {
   const uint32_t n_sets = (uint32_t)c->set_valid.size();
+  if (c->tex_dirty || c->dr_dirty || c->models_dirty || (c->kp_dirty && c->n_kp) || c->n_table_sets != n_sets) {
+    // the device tables are rewritten (and may be reallocated) below: batches
+    // in flight still read them
+    const int rc = drain(c);
+    if (rc) return rc;
+  }
   const bool tex_changed = c->tex_dirty;
   const bool cls_dirty = c->tex_dirty || c->dr_dirty || c->n_table_sets != n_sets || !c->acls.p;
   std::vector<TexDesc> td(c->textures.size());
@@ -532,19 +600,24 @@ static int sync_scene_state(csg_ctx* c) {
 
 static int ensure_work(csg_ctx* c) {
   const uint32_t maxF = c->chain_frames;   // work buffers hold one launch chain
-  if (c->work_frames == maxF && c->rec_cap) return CSG_OK;
-  if (!c->rec_cap) {
+  if (c->work_frames == maxF && c->rec_cap && c->bin_cap) return CSG_OK;
+  {  // buffers are reallocated below
+    const int rc = drain(c);
+    if (rc) return rc;
+  }
+  if (!c->rec_cap)
     c->rec_cap = c->cfg.records_per_frame ? c->cfg.records_per_frame
                                           : (uint32_t)std::min<uint64_t>(c->n_tris_total + c->n_tris_total / 8 + 4096,
                                                                          0x7FFFFFFFull);
+  if (!c->bin_cap)
     c->bin_cap = c->cfg.bins_per_frame ? c->cfg.bins_per_frame
                                        : (uint32_t)std::min<uint64_t>(3ull * c->rec_cap + 16ull * c->n_tiles,
                                                                       0x7FFFFFFFull);
-  }
-  const size_t npx = (size_t)c->cfg.width * c->cfg.height;
   HIP_TRY(c, c->frames.alloc(c->cfg.max_frames));   // the whole batch's frame records
-  if (!c->h_frames)
-    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_frames), sizeof(FrameDev) * c->cfg.max_frames));
+  for (uint32_t k = 0; k < csg_ctx::kStaging; ++k)
+    if (!c->h_stage[k])
+      HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_stage[k]), sizeof(FrameDev) * c->cfg.max_frames));
+  HIP_TRY(c, c->fset.alloc(maxF));
   HIP_TRY(c, c->clip.alloc((size_t)maxF * c->n_inst * 12));
   HIP_TRY(c, c->pv.alloc((size_t)maxF * 12));
   HIP_TRY(c, c->cam.alloc((size_t)maxF * kCamFloats));
@@ -555,9 +628,6 @@ static int ensure_work(csg_ctx* c) {
   HIP_TRY(c, c->tile_off.alloc((size_t)maxF * (c->n_tiles + 1)));
   HIP_TRY(c, c->tile_fill.alloc((size_t)maxF * c->n_tiles));
   HIP_TRY(c, c->bins.alloc((size_t)maxF * c->bin_cap));
-  HIP_TRY(c, c->overflow.alloc(16));
-  HIP_TRY(c, hipMemset(c->overflow.p, 0, 16 * sizeof(uint32_t)));
-  (void)npx;
   c->work_frames = maxF;
   return CSG_OK;
 }
@@ -579,6 +649,10 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "render: no scene uploaded");
   if (!frames || !out || F == 0 || F > c->cfg.max_frames)
     return c->fail(CSG_ERR_INVALID, "render: need 1..%u frames", c->cfg.max_frames);
+  // One set of work buffers per context: work queued on another stream must
+  // finish before this batch reuses them.
+  if (c->last_stream && c->last_stream != st) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+  c->last_stream = st;
   int rc = sync_scene_state(c);
   if (rc) return rc;
   rc = ensure_work(c);
@@ -601,11 +675,19 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     dframes = reinterpret_cast<const FrameDev*>(frames);
   } else {
     static_assert(sizeof(FrameDev) == sizeof(csg_frame), "frame layout");
-    memcpy(c->h_frames, frames, sizeof(FrameDev) * F);
-    HIP_TRY(c, hipMemcpyAsync(c->frames.p, c->h_frames, sizeof(FrameDev) * F, hipMemcpyHostToDevice, st));
+    const uint32_t slot = c->stage_next;
+    c->stage_next = (slot + 1) % csg_ctx::kStaging;
+    if (c->stage_busy[slot]) HIP_TRY(c, hipEventSynchronize(c->stage_ev[slot]));   // its last H2D copy is done
+    memcpy(c->h_stage[slot], frames, sizeof(FrameDev) * F);
+    HIP_TRY(c, hipMemcpyAsync(c->frames.p, c->h_stage[slot], sizeof(FrameDev) * F, hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipEventRecord(c->stage_ev[slot], st));
+    c->stage_busy[slot] = true;
     dframes = c->frames.p;
   }
   b.frames = dframes;
+  b.fset = c->fset.p;
+  b.n_sets = (uint32_t)c->set_valid.size();    // = sets in the models, materials and lights tables
+  b.n_kp_sets = (uint32_t)c->kp_valid.size();
   b.models = c->models.p;
   b.mats = c->set_mats.p;
   b.lights = c->lights.p;
@@ -680,7 +762,6 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * Fc * kCounterStride, st));
     HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
     HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
-    if (c0 == 0) HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), st));
     if (want_kp) HIP_TRY(c, hipMemsetAsync(bc.kp_tiles, 0, sizeof(uint32_t) * Fc * bc.tile_words, st));
     launch_init_stats(bc, Fc, st);
     if (c->timing) {
@@ -730,30 +811,28 @@ int csg_render_batch_async(csg_ctx* c, const csg_frame* frames, uint32_t n_frame
 
 int csg_synchronize(csg_ctx* c) {
   if (!c) return CSG_ERR_INVALID;
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  uint32_t ov = 0;
-  if (c->overflow.p) HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
-  if ((c->dbg & 512u) && c->overflow.p) {   // profiling counters, cumulative since the work buffers were sized
-    uint32_t ctr[16];
-    HIP_TRY(c, hipMemcpy(ctr, c->overflow.p, sizeof(ctr), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u alpha_fail %u alpha_pass %u early_z %u "
-            "wide_rows %u\n", ctr[1], ctr[2], ctr[3], ctr[4], ctr[5], ctr[6], ctr[7], ctr[8]);
-  }
-  if (ov)
-    return c->fail(CSG_ERR_OVERFLOW, "work buffer overflow (flags %u): records_per_frame=%u bins_per_frame=%u", ov,
-                   c->rec_cap, c->bin_cap);
-  return CSG_OK;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const int rc = drain(c);
+  if (rc) return rc;
+  return take_flags(c, nullptr);
 }
 
 int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out) {
   if (!c) return CSG_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  // an earlier asynchronous batch that overflowed is reported, not lost
+  int rc = csg_synchronize(c);
+  if (rc) return rc;
   for (int attempt = 0; attempt < 6; ++attempt) {
-    int rc = csg_render_batch_async(c, frames, n_frames, 0, out, nullptr);
+    rc = csg_render_batch_async(c, frames, n_frames, 0, out, nullptr);
     if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     uint32_t ov = 0;
     HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
     if (!ov) return CSG_OK;
+    HIP_TRY(c, hipMemset(c->overflow.p, 0, 4));
+    if (ov & (kOvBadSet | kOvBadKpSet))   // host frames are validated before launch: cannot happen
+      return c->fail(CSG_ERR_DEVICE, "render: unexpected set error flags %u", ov);
     // grow the overflowed capacity and re-render (results are a pure function
     // of inputs): at least double it, or size it from the last launch chain's
     // counters (records counted past the cap; bin totals of the records kept)
@@ -771,9 +850,9 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
     auto grow = [](uint32_t cap, uint32_t need) {
       return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * cap, need + need / 8ull + 1024ull), 0x7FFFFFFFull);
     };
-    if (ov & 1u) c->rec_cap = grow(c->rec_cap, need_rec);
-    if (ov & 2u) c->bin_cap = grow(c->bin_cap, need_bin);
-    if (ov & 1u) c->bin_cap = grow(c->bin_cap, 0);   // more records: more bin entries too
+    if (ov & kOvRecords) c->rec_cap = grow(c->rec_cap, need_rec);
+    if (ov & kOvBins) c->bin_cap = grow(c->bin_cap, need_bin);
+    if (ov & kOvRecords) c->bin_cap = grow(c->bin_cap, 0);   // more records: more bin entries too
     c->work_frames = 0;
   }
   return c->fail(CSG_ERR_OVERFLOW, "work buffers overflowed after growth");
@@ -782,7 +861,10 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
 int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
   if (!c || !st) return CSG_ERR_INVALID;
   memset(st, 0, sizeof(*st));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  {
+    const int rc = drain(c);
+    if (rc) return rc;
+  }
   const uint32_t F = c->last_F;
   st->frames = F;
   if (!F) return CSG_OK;
@@ -811,7 +893,10 @@ int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
 
 int csg_timing_reset(csg_ctx* c) {
   if (!c) return CSG_ERR_INVALID;
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  {
+    const int rc = drain(c);
+    if (rc) return rc;
+  }
   c->ring_count = 0;
   return CSG_OK;
 }

@@ -76,8 +76,17 @@ struct SceneDev {
   uint32_t dbg;                // ablation switches (CSG_DEBUG; 0 in production)
 };
 
+// Bits of overflow[0] (sticky until csg_synchronize / csg_render_batch reads them)
+constexpr uint32_t kOvRecords = 1u;      // a frame emitted more raster records than rec_cap
+constexpr uint32_t kOvBins = 2u;         // a frame's tile-bin entries exceeded bin_cap
+constexpr uint32_t kOvBadSet = 4u;       // device frame named a transform set >= n_sets (rendered with set 0)
+constexpr uint32_t kOvBadKpSet = 8u;     // device frame named a keypoint set >= n_kp_sets (keypoints vis 0)
+
 struct BatchDev {
   const FrameDev* frames;      // [F]
+  uint32_t* fset;              // [F] the frame's transform set, range-checked by k_clip (every later kernel reads this)
+  uint32_t n_sets;             // transform sets resident (models / mats / lights tables)
+  uint32_t n_kp_sets;          // keypoint sets resident
   const float* models;         // [n_sets][I][16]
   const MatDesc* mats;         // [n_sets][n_mat] materials with the set's texture swaps applied
   const LightDev* lights;      // [n_sets]

@@ -306,8 +306,13 @@ __global__ __launch_bounds__(256) void k_clip(SceneDev s, BatchDev b) {
   const uint32_t f = blockIdx.y;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const FrameDev& fr = b.frames[f];
+  // A device-side frame record can name any set: out-of-range sets render with
+  // set 0 and raise kOvBadSet (csg_synchronize reports it); every later kernel
+  // reads the checked set from b.fset.
+  const uint32_t raw = fr.xform_set;
+  const uint32_t set = raw < b.n_sets ? raw : 0u;
   if (i < s.n_inst) {
-    const float* M = b.models + ((size_t)fr.xform_set * s.n_inst + i) * 16;
+    const float* M = b.models + ((size_t)set * s.n_inst + i) * 16;
     float m[16], vm[16], c[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) m[k] = M[k];
@@ -322,6 +327,8 @@ __global__ __launch_bounds__(256) void k_clip(SceneDev s, BatchDev b) {
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    b.fset[f] = set;
+    if (raw >= b.n_sets) atomicOr(b.overflow, kOvBadSet);
     float pv[16];
     mat4_mul(fr.proj, fr.view, pv);
     float* o = b.pv + (size_t)f * 12;
@@ -568,7 +575,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
         if (!h.ok) {
           nrec = 0;
         } else {
-          const MatDesc mat = b.mats[(size_t)b.frames[f].xform_set * b.n_mat + m.material];
+          const MatDesc mat = b.mats[(size_t)b.fset[f] * b.n_mat + m.material];
           float uv[6] = {0, 0, 0, 0, 0, 0};
           if (mat.alpha_test && m.has_uv) {
             const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
@@ -1153,7 +1160,7 @@ struct ShadeEntry {
 __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b, uint32_t f, uint32_t uid,
                                             ShadeEntry& e) {
   const uint32_t i = uid >> kUidShift, t = uid & (kMaxTrisPerMesh - 1u);
-  const uint32_t set = b.frames[f].xform_set;
+  const uint32_t set = b.fset[f];
   const InstDesc m = s.inst[i];
   const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
   float p[9];
@@ -1341,7 +1348,7 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
   const int py = oy + ly, px0 = ox + lx0;
   if (py >= (int)s.H) return;
   const size_t o = (size_t)f * s.W * s.H + (size_t)py * s.W + px0;
-  const uint32_t sky = b.lights[b.frames[f].xform_set].sky & 0xFFFFFFu;
+  const uint32_t sky = b.lights[b.fset[f]].sky & 0xFFFFFFu;
   const float nan = __builtin_nanf("");
   if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
     if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(-1, -1, -1, -1);
@@ -1452,7 +1459,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   uint32_t pend = 0;                 // bit k: pixel k still to shade
   uint32_t inmask = 0;               // bit k: pixel k lies inside the frame
   {
-    const uint32_t sky = b.lights[b.frames[f].xform_set].sky & 0xFFFFFFu;
+    const uint32_t sky = b.lights[b.fset[f]].sky & 0xFFFFFFu;
     const unsigned long long bgword = (unsigned long long)sky | (0xFFFFFFFFull << 32);   // id -1
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1678,11 +1685,21 @@ __global__ __launch_bounds__(256) void k_keypoints(SceneDev s, BatchDev b) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= b.n_kp) return;
   const float* pv = b.pv + (size_t)f * 12;
-  const float* p = b.kp + ((size_t)b.frames[f].xform_set * b.n_kp + k) * 3;
+  const size_t o = (size_t)f * b.n_kp + k;
+  const uint32_t kset = b.frames[f].xform_set;
+  if (kset >= b.n_kp_sets) {   // device frame without keypoints for its set: nothing projected
+    b.kp_uv[o * 2 + 0] = -1.0f;
+    b.kp_uv[o * 2 + 1] = -1.0f;
+    b.kp_vis[o] = 0;
+    b.kp_pix[o] = 0xFFFFFFFFu;
+    b.kp_w[o] = INFINITY;
+    if (k == 0) atomicOr(b.overflow, kOvBadKpSet);
+    return;
+  }
+  const float* p = b.kp + ((size_t)kset * b.n_kp + k) * 3;
   float u, v;
   int vis, px, py;
   project_one(pv, p, (float)s.W, (float)s.H, s.near_clip, u, v, vis, px, py);
-  const size_t o = (size_t)f * b.n_kp + k;
   b.kp_uv[o * 2 + 0] = u;
   b.kp_uv[o * 2 + 1] = v;
   b.kp_vis[o] = vis;

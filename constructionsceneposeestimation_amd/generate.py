@@ -52,22 +52,50 @@ def _write_pointcloud(path: str, points: np.ndarray, rgb: np.ndarray) -> None:
     fileio.write_pointcloud_txt(path, points, rgb)
 
 
+def _atomic(path: str, fn, *args) -> None:
+    """Write through ``path + '.tmp'`` and rename: a crash never leaves a
+    truncated file under the final name."""
+    tmp = path + ".tmp"
+    fn(tmp, *args)
+    os.replace(tmp, path)
+
+
+def _write_frame(files, label: dict, label_path: str) -> None:
+    """Every file of one frame, then its label JSON: the label is the resume
+    marker (generate_construction_data.py:1357-1367 scans labels/), so it
+    appears only once the frame's other files are complete."""
+    for path, fn, args in files:
+        _atomic(path, fn, *args)
+    _atomic(label_path, save_label_json, label)
+
+
+def default_writers() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS") or 0)   # the box's CPU share, when set
+    return max(1, min(n, omp) if omp else n)
+
+
 def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 30,
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
-             width: Optional[int] = None, height: Optional[int] = None, writers: int = 8,
+             width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
              resume: bool = True, normals: bool = False) -> dict:
     wl = Workload(workload, seed=seed, width=width, height=height)
     for d in ("rgb", "labels", "depth", "pointcloud", "normals", "logs"):
         os.makedirs(os.path.join(out_dir, d), exist_ok=True)
     if resume:
         frames = [f for f in frames if not os.path.exists(os.path.join(out_dir, "labels", f"label_{f:06d}.json"))]
+    depth = depth or depth_csv
     log = QualityLog(os.path.join(out_dir, "logs"))
     r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
     intr = wl.intr
     want = (["rgb", "instance", "keypoints", "stats"] + (["depth"] if depth else [])
             + (["points"] if pointcloud else []) + (["normals"] if normals else []))
     pose_cache = {}
-    pool = ThreadPoolExecutor(max_workers=writers)
+    n_writers = writers or default_writers()
+    pool = ThreadPoolExecutor(max_workers=n_writers)
     pending = []
     for s0 in range(0, len(frames), batch):
         fb = frames[s0:s0 + batch]
@@ -91,26 +119,25 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                                out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
                                wl.kp_table, wl.height, wl.width)
             log.frame(lab["num_objects"], out["depth"][k] if "depth" in out else None, out["keypoints_vis"][k])
-            pending.append(pool.submit(_write_png, os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), out["rgb"][k]))
-            pending.append(pool.submit(fileio.write_npy,
-                                       os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"),
-                                       out["instance"][k]))
-            pending.append(pool.submit(save_label_json, lab, os.path.join(out_dir, "labels", f"label_{f:06d}.json")))
+            files = [(os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), _write_png, (out["rgb"][k],)),
+                     (os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"), fileio.write_npy,
+                      (out["instance"][k],))]
             if depth:
-                pending.append(pool.submit(fileio.write_npy, os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"),
-                                           out["depth"][k]))
+                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"), fileio.write_npy,
+                              (out["depth"][k],)))
                 if depth_csv:
-                    pending.append(pool.submit(fileio.write_depth_csv,
-                                               os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), out["depth"][k]))
+                    files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), fileio.write_depth_csv,
+                                  (out["depth"][k],)))
             if pointcloud:
-                pending.append(pool.submit(_write_pointcloud, os.path.join(out_dir, "pointcloud",
-                                                                           f"pointcloud_{f:06d}.txt"),
-                                           out["points"][k], out["rgb"][k]))
+                files.append((os.path.join(out_dir, "pointcloud", f"pointcloud_{f:06d}.txt"), _write_pointcloud,
+                              (out["points"][k], out["rgb"][k])))
             if normals:
-                pending.append(pool.submit(fileio.write_npy,
-                                           os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), out["normals"][k]))
+                files.append((os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), fileio.write_npy,
+                              (out["normals"][k],)))
+            pending.append(pool.submit(_write_frame, files, lab,
+                                       os.path.join(out_dir, "labels", f"label_{f:06d}.json")))
         # bound the queue so host memory stays flat
-        while len(pending) > 64 * max(writers, 1):
+        while len(pending) > 4 * n_writers:
             pending.pop(0).result()
     for p in pending:
         p.result()

@@ -29,12 +29,17 @@ from .scene.model import Scene
 from .scene.proxies import COCO_JOINTS, HumanRig, add_proxies, pose_humans
 
 WORKLOADS = {
-    "C1": dict(scene="cone", width=256, height=256, outputs=("rgb", "instance", "depth")),
-    "C2": dict(scene="world2", width=1920, height=1080, outputs=("rgb", "instance")),
-    "C3": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints")),
-    "C4": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints"), dr=True),
+    "C1": dict(scene="cone", width=256, height=256, outputs=("rgb", "instance", "depth"),
+               title="TrafficCone mesh alone"),
+    "C2": dict(scene="world2", width=1920, height=1080, outputs=("rgb", "instance"),
+               title="world2.usd static (stands in for the missing world1.usd), scheduled camera poses"),
+    "C3": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints"),
+               title="world2.usd + crane/dumper/4 rigged-human proxies"),
+    "C4": dict(scene="world2_people", width=1920, height=1080, outputs=("rgb", "instance", "keypoints"), dr=True,
+               title="world2.usd + proxies, per-epoch lighting/texture/layout/pose DR"),
     "C5": dict(scene="world2_people", width=3840, height=2160,
-               outputs=("rgb", "instance", "depth", "normals", "points", "keypoints")),
+               outputs=("rgb", "instance", "depth", "normals", "points", "keypoints"),
+               title="world2.usd + crane/dumper/people proxies"),
 }
 
 

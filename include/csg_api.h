@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 5
+#define CSG_ABI_VERSION 6
 
 typedef enum {
   CSG_OK = 0,
@@ -156,12 +156,27 @@ int csg_set_dr_textures(csg_ctx* ctx, uint32_t set_id, const int32_t* texture_pe
 /* Render n_frames (<= max_frames) frames; synchronous.  A work buffer that
  * overflows (records or bin entries past the configured caps) is grown from
  * the device counters and the batch rendered again, up to 6 attempts; the
- * results do not depend on the caps. */
+ * results do not depend on the caps.  An overflow left by an earlier
+ * asynchronous batch is reported first (CSG_ERR_OVERFLOW), as by
+ * csg_synchronize. */
 int csg_render_batch(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out);
 /* Same, enqueued on `stream` (a hipStream_t, NULL = context stream); frames
- * may be a device pointer when frames_on_device = 1.  Returns after enqueue. */
+ * may be a device pointer when frames_on_device = 1.  Returns after enqueue;
+ * the work buffers are not grown.  Host frame records are staged through a
+ * ring of pinned buffers, so the caller may reuse `frames` at once.  A batch
+ * on a different stream than the previous one waits for that stream first
+ * (one set of work buffers per context).  Device frame records are checked on
+ * the device: a transform set >= the sets uploaded renders with set 0, a
+ * keypoint set never uploaded projects nothing, and both are reported by the
+ * next csg_synchronize (CSG_ERR_INVALID).  Sets inside the range that were
+ * never uploaded hold zero transforms (nothing is drawn). */
 int csg_render_batch_async(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames,
                            int32_t frames_on_device, const csg_outputs* out, void* stream);
+/* Wait for every batch enqueued so far (context stream and the caller's
+ * stream of the last batch).  Overflow and device-set errors are sticky
+ * across asynchronous batches: any batch since the last csg_synchronize /
+ * csg_render_batch that truncated its records or bin lists makes this return
+ * CSG_ERR_OVERFLOW (then the flag is cleared). */
 int csg_synchronize(csg_ctx* ctx);
 int csg_get_batch_stats(csg_ctx* ctx, csg_batch_stats* st);
 

@@ -1,0 +1,98 @@
+"""bench.py's host-side arithmetic (CPU): rank sharding of the timed steps,
+the verified sample, the max-over-ranks elapsed time (gloo, world size 2)
+and the roofline / baseline bookkeeping."""
+import os
+import socket
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_step_frames_are_disjoint_and_fixed_per_rank(world):
+    F, W, K = 40, 2, 3
+    per_rank = [bench.rank_frames(r, world, W + K, F) for r in range(world)]
+    for r, fr in enumerate(per_rank):
+        assert len(fr) == (W + K) * F                      # weak scaling: fixed work per rank
+        assert all((f // 10) % world == r for f in fr)     # the rank's own epochs only
+        assert bench.timed_frames(fr, W, K, F) == fr[W * F:]
+    flat = [f for fr in per_rank for f in fr]
+    assert len(set(flat)) == len(flat)                     # no frame rendered twice
+
+
+def test_sample_frames_lie_in_the_last_timed_step():
+    F, W, K = 240, 3, 20
+    idx = bench.verify_sample_indices(F, 32)
+    assert len(idx) == 32 and len(set(idx)) == 32
+    assert idx[0] == 0 and idx[-1] == F - 1 and all(0 <= k < F for k in idx)
+    assert bench.verify_sample_indices(F, 0) == []
+    assert bench.verify_sample_indices(5, 9) == [0, 1, 2, 3, 4]
+    fr = bench.rank_frames(0, 1, W + K, F)
+    timed = bench.timed_frames(fr, W, K, F)
+    last = timed[(K - 1) * F:]
+    assert all(last[k] in timed for k in idx)
+
+
+def test_value_is_aggregate_over_ranks():
+    assert bench.aggregate_value(steps=20, frames_per_step=240, world=8, elapsed_max=2.0) == 20 * 240 * 8 / 2.0
+
+
+def test_roofline_formula_follows_survey_8d():
+    M = 10 ** 6
+    r = bench.roofline(b_geom=1000 * M, b_tex=200 * M, b_out=300 * M, frames_per_launch=10, raster_ms=2.0,
+                       setup_ms=1.0, records_per_frame=5 * M, fps=1000.0, traffic={"k_raster": 99})
+    b_frame = 1500 * M
+    assert r["bytes_per_launch"] == 10 * b_frame
+    assert r["achieved"] == pytest.approx(10 * b_frame / 2e-3 / 1e9, rel=1e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, rel=1e-3)
+    assert r["traffic"] == 99 and r["bound"] == "hbm" and r["unit"] == "GB/s"
+    ks = {k["kernel"]: k for k in r["kernels"]}
+    assert ks["k_raster"]["bytes_per_launch"] == 10 * (200 + 300) * M
+    assert ks["k_setup"]["bytes_per_launch"] == 10 * (1000 + 5 * bench.RECORD_BYTES) * M
+    assert r["frame_level"]["frac"] == pytest.approx(1000.0 * b_frame / (bench.HBM_PEAK_GBS * 1e9), rel=1e-3)
+
+
+def test_median_timing_runs_warmup_then_five():
+    calls = []
+    t = bench.median_time(lambda: calls.append(1), runs=5, warmup=1)
+    assert len(calls) == 6 and t >= 0.0
+
+
+def test_cpu_description_is_recorded():
+    assert bench.available_cpus() >= 1
+    assert isinstance(bench.cpu_model(), str) and bench.cpu_model()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = bench.max_over_ranks(0.5 + rank, world)
+    tot = bench.sum_over_ranks([4, rank], world)
+    if rank == 0:
+        with open(out, "w") as fh:
+            fh.write(repr((got, tot)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_elapsed_is_max_and_counts_sum_over_ranks_gloo(tmp_path):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "res.txt")
+    mp.spawn(_rank_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got, tot = eval(open(out).read())
+    assert got == 1.5 and tot == [8, 1]

@@ -5,8 +5,8 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-R=${ROUND:-r01}
-ARGS=${BENCH_ARGS:---steps 6 --warmup 1 --cpu-sample 0 --pcie-steps 0 --stats-steps 0}
+R=${ROUND:-r02}
+ARGS=${BENCH_ARGS:---steps 6 --warmup 1 --verify-frames 0 --pcie-steps 0 --stats-steps 0}
 OUT=gpurun_out/pmc_$R
 mkdir -p $OUT
 run() {  # name counters...

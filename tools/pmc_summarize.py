@@ -49,12 +49,26 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
                 o["valu_lane_util"] = o["SQ_THREAD_CYCLES_VALU"] / (o["SQ_ACTIVE_INST_VALU"] * 64)
     print(json.dumps(out, indent=1, sort_keys=True))
     if write_profile and "k_raster" in out and "hbm_bytes_per_launch" in out["k_raster"]:
+        # the bench line of a pass names the workload, frames per launch and B_frame it ran
+        line = None
+        for f in sorted(glob.glob(os.path.join(root, "*.json"))):
+            try:
+                line = json.load(open(f))
+                break
+            except Exception:
+                continue
         here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        prof = {"workload": workload, "frames_per_launch": frames_per_launch,
-                "k_raster_bytes_per_launch": int(out["k_raster"]["hbm_bytes_per_launch"]),
+        prof = {"workload": line["config"]["workload"].split(":")[0] if line else workload,
+                "frames_per_launch": line["config"]["frames_per_launch"] if line else frames_per_launch,
+                "B_frame": line["roofline"]["frame_level"]["B_frame"] if line else None,
+                "bytes_per_launch": {k: int(out[k]["hbm_bytes_per_launch"]) for k in ("k_raster", "k_setup")
+                                     if "hbm_bytes_per_launch" in out.get(k, {})},
                 "k_raster_fetch_size_kb": out["k_raster"]["FETCH_SIZE"],
                 "k_raster_write_size_kb": out["k_raster"]["WRITE_SIZE"],
-                "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1; KB=1024 B",
+                "correction": "FETCH_SIZE x2 (gfx950 counts 64 B per 128-B read request: TCC_EA0_RDREQ x 64 B; "
+                              "MI355X_MICROARCH.md §HBM), WRITE_SIZE x1; KB = 1024 B. Basis for k_raster's access "
+                              "mix: profiles/r01/fetch_calibration.json (4-B gathers and 112-B records also cost "
+                              "one 128-B request per touched line)",
                 "k_raster_valu_busy": out["k_raster"].get("valu_busy"),
                 "k_raster_valu_lane_util": out["k_raster"].get("valu_lane_util"),
                 "source": os.path.basename(os.path.normpath(root))}
