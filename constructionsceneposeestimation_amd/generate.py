@@ -66,7 +66,7 @@ def _write_frame(files, label: dict, label_path: str) -> None:
     appears only once the frame's other files are complete."""
     for path, fn, args in files:
         _atomic(path, fn, *args)
-    _atomic(label_path, save_label_json, label)
+    _atomic(label_path, lambda path, lab: save_label_json(lab, path), label)
 
 
 def default_writers() -> int:
