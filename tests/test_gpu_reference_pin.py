@@ -17,7 +17,8 @@ flipped).
 
 Stated tolerances (float32 GPU arithmetic vs the reference's float64):
 * points: |delta| <= 2e-4 m + 2e-6 x distance, pixel selection and RGB exact;
-* keypoint uv: <= 2e-3 px; visibility class exact away from the image border.
+* keypoint uv: <= 2e-3 px x max(1, 2 m / Z) (Z = distance to the image plane);
+  visibility class exact away from the image border and pixel boundaries.
 """
 import numpy as np
 import pytest
@@ -85,7 +86,9 @@ def test_gpu_keypoints_match_reference_pinhole():
         u = fx * X[front] / Z[front] + cx
         v = fy * Y[front] / Z[front] + cy
         uv = out["keypoints_uv"][front].astype(np.float64)
-        assert np.abs(uv - np.stack([u, v], 1)).max() <= 2e-3
+        # float32 view-transform rounding (~1e-7 x |p|) grows as 1/Z for keypoints close to the camera
+        tol = 2e-3 * np.maximum(1.0, 2.0 / Z[front])
+        assert (np.abs(uv - np.stack([u, v], 1)).max(axis=1) <= tol).all()
         vis = out["keypoints_vis"]
         assert (vis[Z < 0.5 - 1e-4] == 0).all()
         Wd, Hd = p["width"], p["height"]
