@@ -13,6 +13,13 @@ the asset files are LFS pointers).  These proxies give config C3/C4 the same
   5); a pose is a set of instance transforms, so re-posing a human per
   randomisation epoch is a transform upload, not a mesh upload.
 
+Tessellation follows SURVEY §8(d) ("procedural rigged humans, ~20k tris
+each"): a human is 20,160 triangles (nine 1,248-triangle limb tubes, a
+3,072-triangle torso, a 4,992-triangle head, two 432-triangle feet); the
+crane (~36k) and the dumper (~25k) are built from the same finely
+tessellated primitives, so their triangle counts are those of detailed
+proxies rather than of a handful of boxes.
+
 Everything is generated deterministically from code: no asset files.
 """
 from __future__ import annotations
@@ -80,6 +87,79 @@ def unit_sphere(nu: int = 20, nv: int = 14) -> Tuple[np.ndarray, np.ndarray]:
     for j in range(nu):
         t.append((last, base + (j + 1) % nu, base + j))
     return v, np.array(t, np.uint32)
+
+
+def grid_box(n: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Cube [-0.5,0.5]^3 whose faces are n x n quads (12 n^2 triangles)."""
+    g = np.linspace(-0.5, 0.5, n + 1)
+    verts, tris = [], []
+    for axis in range(3):
+        ua, va = [a for a in range(3) if a != axis]
+        for sign in (-0.5, 0.5):
+            base = sum(len(v) for v in verts)
+            vv, uu = np.meshgrid(g, g, indexing="ij")
+            p = np.zeros(((n + 1) * (n + 1), 3))
+            p[:, axis] = sign
+            p[:, ua] = uu.reshape(-1)
+            p[:, va] = vv.reshape(-1)
+            verts.append(p)
+            j, i = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+            a = (base + j * (n + 1) + i).reshape(-1)
+            b, c, d = a + 1, a + n + 1, a + n + 2
+            t = np.stack([a, b, d, a, d, c], 1).reshape(-1, 3) if sign > 0 else \
+                np.stack([a, d, b, a, c, d], 1).reshape(-1, 3)
+            tris.append(t)
+    return np.concatenate(verts).astype(np.float32), np.concatenate(tris).astype(np.uint32)
+
+
+def unit_tube(seg: int, rings: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Radius 1, z from 0 to 1, `rings` bands of `seg` quads plus capped ends
+    (2 seg (rings + 1) triangles)."""
+    ang = 2 * np.pi * np.arange(seg) / seg
+    ring = np.stack([np.cos(ang), np.sin(ang)], 1)
+    z = np.repeat(np.arange(rings + 1) / rings, seg)
+    v = np.concatenate([np.c_[np.tile(ring, (rings + 1, 1)), z], [[0, 0, 0], [0, 0, 1]]]).astype(np.float32)
+    i = np.arange(seg)
+    j = (i + 1) % seg
+    t = []
+    for r in range(rings):
+        a0, a1 = r * seg, (r + 1) * seg
+        t += [np.stack([a0 + i, a0 + j, a1 + j], 1), np.stack([a0 + i, a1 + j, a1 + i], 1)]
+    c0, c1 = (rings + 1) * seg, (rings + 1) * seg + 1
+    t += [np.stack([np.full(seg, c0), j, i], 1), np.stack([np.full(seg, c1), rings * seg + i, rings * seg + j], 1)]
+    return v, np.concatenate(t).astype(np.uint32)
+
+
+def unit_torus(seg: int, rseg: int, r: float) -> Tuple[np.ndarray, np.ndarray]:
+    """Ring radius 1 about z, tube radius r (2 seg rseg triangles)."""
+    a = 2 * np.pi * np.arange(seg) / seg
+    b = 2 * np.pi * np.arange(rseg) / rseg
+    A, B = np.meshgrid(a, b, indexing="ij")
+    rr = 1.0 + r * np.cos(B)
+    v = np.stack([rr * np.cos(A), rr * np.sin(A), r * np.sin(B)], -1).reshape(-1, 3).astype(np.float32)
+    I, J = np.meshgrid(np.arange(seg), np.arange(rseg), indexing="ij")
+    p00 = I * rseg + J
+    p10 = ((I + 1) % seg) * rseg + J
+    p01 = I * rseg + (J + 1) % rseg
+    p11 = ((I + 1) % seg) * rseg + (J + 1) % rseg
+    t = np.stack([p00, p10, p11, p00, p11, p01], -1).reshape(-1, 3)
+    return v, t.astype(np.uint32)
+
+
+# tessellations used by the proxies (name -> mesh); keys double as mesh names
+PRIMITIVES = {
+    "box": unit_box,
+    "cyl": unit_cylinder,
+    "sphere": unit_sphere,
+    "box6": lambda: grid_box(6), "box8": lambda: grid_box(8), "box10": lambda: grid_box(10),
+    "box12": lambda: grid_box(12), "box16": lambda: grid_box(16), "box20": lambda: grid_box(20),
+    "tube12x8": lambda: unit_tube(12, 8), "tube16x2": lambda: unit_tube(16, 2), "tube24x8": lambda: unit_tube(24, 8),
+    "tube32x4": lambda: unit_tube(32, 4), "tube32x12": lambda: unit_tube(32, 12),
+    "tube48x2": lambda: unit_tube(48, 2), "tube48x12": lambda: unit_tube(48, 12),
+    "tube96x6": lambda: unit_tube(96, 6), "tube128x32": lambda: unit_tube(128, 32),
+    "sphere32x20": lambda: unit_sphere(32, 20), "sphere64x40": lambda: unit_sphere(64, 40),
+    "torus64x24": lambda: unit_torus(64, 24, 0.42), "torus48x12": lambda: unit_torus(48, 12, 0.08),
+}
 
 
 def bone_matrix(a: np.ndarray, b: np.ndarray, radius: float) -> np.ndarray:
@@ -198,25 +278,59 @@ PROXY_MATERIALS = {
     "vest": (0.98, 0.78, 0.05), "skin": (0.80, 0.62, 0.50), "trousers": (0.15, 0.20, 0.35),
 }
 
-# Crane parts: (first-level child name from CRANE_PART_CHILD_MAP, part mesh, local matrix, material)
+# Crane parts: (first-level child name from CRANE_PART_CHILD_MAP, primitive, local matrix, material);
+# several pieces may share a child (one object root each, GDP:110-121).
+_BOOM = X.translate((0, 0, 2.2)) @ X.rot_y(-22)
+_TELE = _BOOM @ X.translate((2.7, 0, 0)) @ X.rot_y(40)
+_TIP = (_TELE @ np.array([2.8, 0.0, 0.0, 1.0]))[:3]
+_HOOK = _TIP + np.array([0.0, 0.0, -1.2])
 _CRANE_PARTS = [
-    ("S104GG03A_SW", "box", box_matrix((0, 0, 0.30), (1.3, 1.0, 0.6)), "crane_grey"),
-    ("S104HZ01KA_SW", "cyl", X.translate((0, 0, 0.6)) @ X.scale((0.17, 0.17, 1.55)), "crane_red"),
-    ("tn__S104EKB_AS_SW_jj7", "box",
-     X.translate((0, 0, 2.2)) @ X.rot_y(-22) @ X.translate((1.35, 0, 0)) @ X.scale((2.9, 0.26, 0.32)), "crane_yellow"),
-    ("S104KZ02KA_SW", "box",
-     X.translate((0, 0, 2.2)) @ X.rot_y(-22) @ X.translate((2.7, 0, 0)) @ X.rot_y(40) @ X.translate((1.1, 0, 0))
-     @ X.scale((2.3, 0.19, 0.23)), "crane_yellow"),
+    # cranebase: chassis block, two outrigger beams with four jacks, slewing ring (6,560 tris)
+    ("S104GG03A_SW", "box16", box_matrix((0, 0, 0.30), (1.3, 1.0, 0.6)), "crane_grey"),
+    ("S104GG03A_SW", "box6", box_matrix((0.45, 0, 0.18), (0.16, 3.0, 0.16)), "crane_yellow"),
+    ("S104GG03A_SW", "box6", box_matrix((-0.45, 0, 0.18), (0.16, 3.0, 0.16)), "crane_yellow"),
+] + [
+    ("S104GG03A_SW", "tube32x4", X.translate((x, y, 0.0)) @ X.scale((0.07, 0.07, 0.35)), "steel")
+    for x in (0.45, -0.45) for y in (1.45, -1.45)
+] + [
+    ("S104GG03A_SW", "tube96x6", X.translate((0, 0, 0.6)) @ X.scale((0.42, 0.42, 0.12)), "crane_grey"),
+    # cranecolumn: column and two lift rams (10,112 tris)
+    ("S104HZ01KA_SW", "tube128x32", X.translate((0, 0, 0.6)) @ X.scale((0.17, 0.17, 1.55)), "crane_red"),
+    ("S104HZ01KA_SW", "tube32x12", bone_matrix((0.25, 0.1, 0.8), (0.6, 0.1, 2.0), 0.05), "steel"),
+    ("S104HZ01KA_SW", "tube32x12", bone_matrix((0.25, -0.1, 0.8), (0.6, -0.1, 2.0), 0.05), "steel"),
+    # craneboom: boom, two hydraulic cylinders, 20 lattice struts (8,384 tris)
+    ("tn__S104EKB_AS_SW_jj7", "box20", _BOOM @ X.translate((1.35, 0, 0)) @ X.scale((2.9, 0.26, 0.32)), "crane_yellow"),
+    ("tn__S104EKB_AS_SW_jj7", "tube32x12", bone_matrix((0.9, 0.17, 2.3), (2.6, 0.17, 1.9), 0.045), "steel"),
+    ("tn__S104EKB_AS_SW_jj7", "tube32x12", bone_matrix((0.9, -0.17, 2.3), (2.6, -0.17, 1.9), 0.045), "steel"),
+] + [
+    ("tn__S104EKB_AS_SW_jj7", "tube16x2",
+     _BOOM @ X.translate((0.2 + 0.25 * k, 0.14 * side, -0.16)) @ X.scale((0.015, 0.015, 0.32)), "steel")
+    for k in range(10) for side in (1.0, -1.0)
+] + [
+    # cranetelescopic: three nested extension sections, hook block and cable (10,648 tris)
+    ("S104KZ02KA_SW", "box16", _TELE @ X.translate((0.6, 0, 0)) @ X.scale((1.2, 0.19, 0.23)), "crane_yellow"),
+    ("S104KZ02KA_SW", "box16", _TELE @ X.translate((1.5, 0, 0)) @ X.scale((1.1, 0.16, 0.2)), "crane_yellow"),
+    ("S104KZ02KA_SW", "box16", _TELE @ X.translate((2.3, 0, 0)) @ X.scale((1.0, 0.13, 0.17)), "crane_yellow"),
+    ("S104KZ02KA_SW", "sphere32x20", X.translate(_HOOK) @ X.scale((0.12, 0.12, 0.12)), "steel"),
+    ("S104KZ02KA_SW", "tube12x8", bone_matrix(_TIP, _HOOK, 0.012), "steel"),
 ]
 
-_DUMPER_PARTS = [
-    ("chassis", "box", box_matrix((0, 0, 0.62), (3.2, 1.5, 0.45)), "dumper_orange"),
-    ("skip", "box", X.translate((0.95, 0, 1.05)) @ X.rot_y(-12) @ X.scale((1.5, 1.65, 0.75)), "dumper_orange"),
-    ("rops", "box", box_matrix((-1.15, 0, 1.55), (0.12, 1.2, 1.4)), "steel"),
-    ("seat", "box", box_matrix((-0.75, 0, 1.05), (0.55, 0.6, 0.45)), "steel"),
+_WHEELS = [(1.0, 0.78), (1.0, -0.78), (-1.0, 0.78), (-1.0, -0.78)]
+_DUMPER_PARTS = [  # (piece, primitive, local matrix, material): 25,728 tris
+    ("chassis", "box20", box_matrix((0, 0, 0.62), (3.2, 1.5, 0.45)), "dumper_orange"),
+    ("skip", "box16", X.translate((0.95, 0, 1.05)) @ X.rot_y(-12) @ X.scale((1.5, 1.65, 0.75)), "dumper_orange"),
+    ("rops_l", "tube24x8", bone_matrix((-1.15, 0.55, 0.85), (-1.15, 0.55, 2.2), 0.05), "steel"),
+    ("rops_r", "tube24x8", bone_matrix((-1.15, -0.55, 0.85), (-1.15, -0.55, 2.2), 0.05), "steel"),
+    ("rops_top", "tube24x8", bone_matrix((-1.15, -0.55, 2.2), (-1.15, 0.55, 2.2), 0.05), "steel"),
+    ("seat", "box8", box_matrix((-0.75, 0, 1.05), (0.55, 0.6, 0.45)), "steel"),
+    ("hood", "box10", box_matrix((-0.2, 0, 1.0), (0.7, 1.2, 0.35)), "dumper_orange"),
+    ("steering", "torus48x12", X.translate((-0.45, 0, 1.5)) @ X.rot_y(-30) @ X.scale((0.18, 0.18, 0.18)), "tyre"),
 ] + [
-    (f"wheel_{i}", "cyl", X.translate((x, y, 0.46)) @ X.rot_x(90) @ X.translate((0, 0, -0.19)) @ X.scale((0.46, 0.46, 0.38)),
-     "tyre") for i, (x, y) in enumerate([(1.0, 0.78), (1.0, -0.78), (-1.0, 0.78), (-1.0, -0.78)])
+    (f"tyre_{i}", "torus64x24", X.translate((x, y, 0.46)) @ X.rot_x(90) @ X.scale((0.36, 0.36, 0.36)), "tyre")
+    for i, (x, y) in enumerate(_WHEELS)
+] + [
+    (f"rim_{i}", "tube48x2", X.translate((x, y, 0.46)) @ X.rot_x(90) @ X.translate((0, 0, -0.15))
+     @ X.scale((0.3, 0.3, 0.3)), "steel") for i, (x, y) in enumerate(_WHEELS)
 ]
 
 # authored placements (world2): crane at the origin, dumper at (-7.37, 0) yawed -92.19 deg,
@@ -238,7 +352,7 @@ def add_proxies(scene: Scene, n_humans: int = 4, crane: bool = True, dumper: boo
     def mesh(kind, material):
         key = (kind, material)
         if key not in mesh_ids:
-            v, t = {"box": unit_box, "cyl": unit_cylinder, "sphere": unit_sphere}[kind]()
+            v, t = PRIMITIVES[kind]()
             scene.meshes.append(Mesh(f"proxy_{kind}_{material}", v, t, np.zeros((0, 2), np.float32),
                                      np.zeros((0, 3), np.uint32), mat(material)))
             mesh_ids[key] = len(scene.meshes) - 1
@@ -299,8 +413,8 @@ def add_proxies(scene: Scene, n_humans: int = 4, crane: bool = True, dumper: boo
         locs = HumanRig.part_locals(J)
         mats = {name: m for name, _, _, _, m in HumanRig.BONES}
         mats.update({"torso": "vest", "head": "skin", "foot_l": "trousers", "foot_r": "trousers"})
-        kinds = {name: "cyl" for name, *_ in HumanRig.BONES}
-        kinds.update({"torso": "box", "head": "sphere", "foot_l": "box", "foot_r": "box"})
+        kinds = {name: "tube48x12" for name, *_ in HumanRig.BONES}
+        kinds.update({"torso": "box16", "head": "sphere64x40", "foot_l": "box6", "foot_r": "box6"})
         parts = []
         for name, local in locs.items():
             parts.append([add_part(o, kinds[name], mats[name], local, frame), name])

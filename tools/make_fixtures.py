@@ -5,7 +5,7 @@ exist on the GPU box).  Outputs under constructionsceneposeestimation_amd/assets
 
 * world2_static.npz — world2.usd.backup decoded by scene/usdc.py: 5 unique
   meshes, 48 instances, 36 labelled objects (23 fence, 11 tree, 2 cone),
-  715,944 triangles, stand-in textures.
+  715,944 triangles, full-resolution stand-in textures.
 * cone.npz — the TrafficCone mesh alone (config C1).
 
 Usage: python tools/make_fixtures.py [/root/reference]
@@ -29,14 +29,8 @@ ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 def main(ref: str = "/root/reference") -> None:
     os.makedirs(ASSETS, exist_ok=True)
     src = os.path.join(ref, "cad_models", "world2.usd.backup")
-    scene = load_crate_scene(src, texture_root=ref, max_texture=1024)
-    # bark stand-in downsampled: a 1600x1300 photo adds MBs and no test value
-    from PIL import Image
-    for t in scene.textures:
-        if t.name.startswith("Bark") and max(t.rgba.shape[:2]) > 512:
-            im = Image.fromarray(t.rgba)
-            r = 512 / max(im.size)
-            t.rgba = np.asarray(im.resize((round(im.size[0] * r), round(im.size[1] * r)), Image.LANCZOS)).copy()
+    # full-resolution stand-in textures (SURVEY §8(d) B_tex: leaf 766x1024 + bark 1600x1300 RGBA8 = 11.46 MB)
+    scene = load_crate_scene(src, texture_root=ref, max_texture=4096)
     assert scene.meta["n_mesh_prims"] == 1060, scene.meta
     assert len(scene.objects) == 36
     assert scene.n_tris_per_frame == 715944
