@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 REPS=${REPS:-1}
 for rep in $(seq $REPS); do
 for e in ${ENVS}; do
-  env ${e//:/ } timeout -k 10 200 python bench.py --cpu-sample 0 --steps ${STEPS:-20} ${BENCH_ARGS} > gpurun_out/abenv.json 2>/dev/null || { echo "$e FAILED"; exit 1; }
+  env ${e//:/ } timeout -k 10 200 python bench.py --verify-frames 0 --steps ${STEPS:-20} ${BENCH_ARGS} > gpurun_out/abenv.json 2>/dev/null || { echo "$e FAILED"; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/abenv.json')); print('$e', d['value'], d['stage_ms_per_step'], d['roofline']['avg_launch_ms'])"
 done
 done
