@@ -47,11 +47,6 @@ struct __attribute__((aligned(16))) Rec {
   uint32_t athr;               // 4 : alpha threshold (keep iff alpha > athr)
 };
 static_assert(sizeof(Rec) == 112, "Rec layout");
-// Rec::y[0] of a record whose coverage k_setup already decided exactly (at
-// most 4x4 pixel centres): Rec::x[0] then holds the covered centres as a bit
-// mask, bit 4j + i = centre (px0 + i, py0 + j).  No vertex reaches this value
-// (|fixed-point coordinates| < 2^28).
-constexpr uint32_t kMaskFlag = 0x80000000u;
 constexpr int kRecGroups = 7;  // 16-B field groups k_raster stages (the 112 B of payload)
 
 struct FrameDev {                // csg_frame mirror
@@ -107,7 +102,7 @@ struct BatchDev {
   uint32_t* tile_fill;         // [F][n_tiles]
   uint32_t* bins;              // [F][bin_cap]
   uint32_t bin_cap;
-  uint32_t* overflow;          // [16]: [0] kOv* bits (sticky); [1..] profiling counters (CSG_DEBUG 512)
+  uint32_t* overflow;          // [16]: [0] bit0 rec, bit1 bins; [1..] profiling counters (CSG_DEBUG 512)
   // outputs (device)
   uint8_t* rgb;                // [F][H][W][3] or null
   int32_t* inst;               // [F][H][W] or null

@@ -59,16 +59,6 @@ namespace csg {
 #ifndef CSG_SMALL_COVER
 #define CSG_SMALL_COVER 4      // records with at most N x N pixel centres get an exact cover test in k_setup (0: off)
 #endif
-#ifndef CSG_MASK_RECORDS
-// small records carry their exact coverage as a bit mask (k_raster's level 1 reads spans from it)
-#define CSG_MASK_RECORDS (CSG_SMALL_COVER > 0 && CSG_SMALL_COVER <= 4)
-#endif
-#ifndef CSG_COARSE_Z
-#define CSG_COARSE_Z 1         // k_raster drops records (1) / and rows (2) entirely behind the z-buffer (raster_block)
-#endif
-#ifndef CSG_CLASS_ORDER
-#define CSG_CLASS_ORDER 1      // level-1 items ordered by record class (mask, small, large)
-#endif
 
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr float kGuardPx = 1048576.0f;
@@ -386,8 +376,6 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
   // fewer record stores, bin entries and raster row items.  Exact in int32:
   // |dx|, |dy| < 2^13 and every centre lies within the vertex extent.
   constexpr int N = CSG_SMALL_COVER;
-  bool masked = false;
-  uint32_t cmask = 0;      // bit 4j + i: centre (px0 + i, py0 + j) covered (N <= 4)
   if (px1 - px0 < N && py1 - py0 < N && xmax - xmin < 8192 && ymax - ymin < 8192) {
     const int32_t cx0 = px0 * 256 + 128, cy0 = py0 * 256 + 128;
     const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
@@ -411,33 +399,17 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
         for (int e = 0; e < 3; ++e) in &= e0[e] + sx[e] * i + sy[e] * j >= 0;
         cols |= in ? 1u << i : 0u;
         rows |= in ? 1u << j : 0u;
-#if CSG_MASK_RECORDS
-        cmask |= in ? 1u << (4 * j + i) : 0u;
-#endif
       }
     }
     if (!cols) return false;
-    const int dx = __ffs(cols) - 1, dy = __ffs(rows) - 1;
     px1 = px0 + 31 - __clz(cols);
-    px0 += dx;
+    px0 += __ffs(cols) - 1;
     py1 = py0 + 31 - __clz(rows);
-    py0 += dy;
-#if CSG_MASK_RECORDS
-    // re-base the mask on the shrunk box: no covered centre lies left of dx
-    // or above dy, so one shift moves every row's bits to its nibble's low end
-    cmask >>= 4 * dy + dx;
-    masked = true;
-#endif
+    py0 += __ffs(rows) - 1;
   }
 #endif
 #pragma unroll
   for (int k = 0; k < 3; ++k) { r.x[k] = x[k]; r.y[k] = y[k]; }
-#if CSG_SMALL_COVER && CSG_MASK_RECORDS
-  if (masked) {            // the vertices are not needed any more: coverage is the mask
-    r.x[0] = (int32_t)cmask;
-    r.y[0] = (int32_t)kMaskFlag;
-  }
-#endif
   r.px0 = (uint16_t)px0; r.py0 = (uint16_t)py0; r.px1 = (uint16_t)px1; r.py1 = (uint16_t)py1;
   return true;
 }
@@ -896,6 +868,12 @@ struct RasterCtx {
 #ifndef CSG_RASTER_FRAME_FAST
 #define CSG_RASTER_FRAME_FAST 0
 #endif
+#ifndef CSG_L1_BITMAP
+#define CSG_L1_BITMAP 1
+#endif
+#ifndef CSG_L2_BITMAP
+#define CSG_L2_BITMAP 1
+#endif
 #ifndef CSG_TILE_SWIZZLE
 #define CSG_TILE_SWIZZLE 2
 #endif
@@ -911,7 +889,7 @@ struct RasterCtx {
 #define CSG_RASTER_ATTR
 #endif
 constexpr int kStage = CSG_STAGE;     // records staged per raster batch (<= kBlock)
-static_assert(kStage <= kBlock && kStage <= 128, "one staged record per thread; 7-bit slot ids");
+static_assert(kStage <= kBlock, "one staged record per thread");
 struct RecImage {
   uint4 q[kRecGroups][kStage];
 };
@@ -948,218 +926,100 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
     const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
     float u, v;
     interp_uv(e, ssum, uv, u, v);
-    // the staged image keeps the record's depth bound in the threshold word's upper half
-    const bool pass = alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)(g6.w & 0xFFu), u, v);
+    const bool pass = alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)g6.w, u, v);
     if (DBG(c.dbg) & 512u) atomicAdd(&c.ctr[pass ? 6 : 5], 1u);   // profiling: alpha tests passed / failed
     if (!pass) return;
   }
   atomicMin(z, key);
 }
 
-struct RasterLds {
-  RecImage img;                         // staged bin records
-  // Coarse z: per tile row, four 8-pixel segments (u16 each) holding the
-  // largest depth part (bits 63..48) of the z-buffer keys in the segment.
-  unsigned long long segs[kTile];
-  uint32_t starts1[kStage];             // bit i: a staged record's rows start at level-1 item i
-  uint16_t before1[kStage + 1];         // records starting before item 32*d
-  uint32_t crec[kStage];                // compact record: slot | first item << 8
-  uint8_t row0[kStage];                 // first tile row of each staged record | 0x80 if small
-  uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
-  uint32_t starts[kBlock];              // bit i: a span starts at level-2 item i (<= 256 spans x 32 px)
-  uint16_t before[kBlock + 1];          // spans starting before item 32*d
-  uint32_t wsum[3 * (kBlock / 64)];     // block scans (three at once in level 1)
-};
-
-// Coarse-z refresh: the segment maxima of the current z-buffer.  Thread t
-// owns pixels 4t..4t+3 (row t/8); threads t and t^1 form one segment.  Other
-// threads may read a segment while it is rewritten: any value it ever held
-// bounds the keys from above (keys only decrease), so stale reads are safe.
-__device__ __forceinline__ void refresh_segs(const unsigned long long* zb, unsigned long long* segs) {
-  const int tid = threadIdx.x;
-  const unsigned long long* p = zb + tid * 4;
-  uint32_t m = max(max((uint32_t)(p[0] >> 32), (uint32_t)(p[1] >> 32)),
-                   max((uint32_t)(p[2] >> 32), (uint32_t)(p[3] >> 32)));
-  m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
-  if (!(tid & 1)) reinterpret_cast<uint16_t*>(segs)[tid >> 1] = (uint16_t)(m >> 16);
-}
-
-// True iff every z-buffer key in tile rows ly0..ly1, columns lx0..lx1 has a
-// depth part below kb16 << 16: a fragment whose depth part is at least that
-// cannot win any of those pixels.
-__device__ __forceinline__ bool segs_behind(const unsigned long long* segs, int ly0, int ly1, int lx0, int lx1,
-                                            uint32_t kb16) {
-  const uint32_t s0 = (uint32_t)lx0 >> 3, ns = ((uint32_t)lx1 >> 3) - s0 + 1u;
-  const unsigned long long keep = ns >= 4u ? ~0ull : ((1ull << (16u * ns)) - 1ull);
-#pragma clang loop unroll(disable)
-  for (int r = ly0; r <= ly1; ++r) {
-    const unsigned long long w = (segs[r] >> (16u * s0)) & keep;
-    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-    const uint32_t m = max(max(lo & 0xFFFFu, lo >> 16), max(hi & 0xFFFFu, hi >> 16));
-    if (m >= kb16) return false;
-  }
-  return true;
-}
-
-// Stage bin entry `idx` into `slot`; returns its row count inside the tile,
-// its first row (| 0x80 if small) and its class for the level-1 order:
-// 0 = exact-mask record, 1 = small (32-bit span arithmetic), 2 = large.
-// With `bound` (coarse z, batches after the first) it also derives a
-// conservative nearest-depth bound over the record's box in the tile: the
-// record is dropped if the depth range rejects all of it or the z-buffer is
-// nearer everywhere in its box; otherwise the bound (top 16 bits of the
-// key's depth part) is kept in the staged threshold word for level 1.
-__device__ __forceinline__ uint32_t stage_record(const RasterCtx& c, const Rec* recs, const uint32_t* bins,
-                                                 uint32_t idx, uint32_t end, uint32_t rec_cap, RasterLds& L,
-                                                 int slot, bool bound, uint32_t& row0, uint32_t& cls) {
+// Stage bin entry `idx` into `slot`; returns its row count inside the tile.
+__device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t* bins, uint32_t idx, uint32_t end,
+                                                 uint32_t rec_cap, RecImage& img, int slot, int ox, int oy,
+                                                 uint32_t& row0) {
   row0 = 0;
-  cls = 2;
   const uint32_t r = (idx < end && slot < kStage) ? bins[idx] : 0xFFFFFFFFu;
   if (r >= rec_cap) return 0;
-  const int ox = c.ox, oy = c.oy;
   const uint4* src = reinterpret_cast<const uint4*>(recs + r);
   uint4 q[kRecGroups];
 #pragma unroll
   for (int k = 0; k < kRecGroups; ++k) q[k] = src[k];
+#pragma unroll
+  for (int k = 0; k < kRecGroups; ++k) img.q[k][slot] = q[k];
   const uint32_t p0 = q[1].z, p1 = q[1].w;            // px0 | py0 << 16, px1 | py1 << 16
   int y0 = max((int)(p0 >> 16), oy), y1 = min((int)(p1 >> 16), oy + kTile - 1);
   const int x0 = max((int)(p0 & 0xFFFFu), ox), x1 = min((int)(p1 & 0xFFFFu), ox + kTile - 1);
-  uint32_t rows = 0;
-  if (x0 <= x1 && y0 <= y1) {
-    if (q[0].w == kMaskFlag) {                        // exact coverage mask from k_setup
-      cls = 0;
-      row0 = (uint32_t)(y0 - oy);
-      rows = (uint32_t)(y1 - y0 + 1);
-    } else {
-      // Rows of the triangle inside this tile's column strip: the y-range of
-      // the triangle clipped to the pixel-centre lines x0..x1, in float
-      // relative to the tile, widened (>> any rounding here); the exact row
-      // spans of level 1 decide coverage, this only drops rows that cannot
-      // have any.
-      const int32_t X[3] = {(int32_t)q[0].x, (int32_t)q[0].y, (int32_t)q[0].z};
-      const int32_t Y[3] = {(int32_t)q[0].w, (int32_t)q[1].x, (int32_t)q[1].y};
-      const float sl = (float)(x0 * 256 + 128), sr = (float)(x1 * 256 + 128);
-      float fx[3], fy[3];
+  if (x0 > x1 || y0 > y1) return 0u;
+  // Rows of the triangle inside this tile's column strip: the y-range of the
+  // triangle clipped to the pixel-centre lines x0..x1, in float relative to
+  // the tile, widened by half a pixel (>> any rounding here); the exact row
+  // spans of level 1 decide coverage, this only drops rows that cannot have any.
+  const int32_t X[3] = {(int32_t)q[0].x, (int32_t)q[0].y, (int32_t)q[0].z};
+  const int32_t Y[3] = {(int32_t)q[0].w, (int32_t)q[1].x, (int32_t)q[1].y};
+  const float sl = (float)(x0 * 256 + 128), sr = (float)(x1 * 256 + 128);
+  float fx[3], fy[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { fx[k] = (float)X[k]; fy[k] = (float)(Y[k] - oy * 256); }
-      float ylo = 1.0e30f, yhi = -1.0e30f;
+  for (int k = 0; k < 3; ++k) { fx[k] = (float)X[k]; fy[k] = (float)(Y[k] - oy * 256); }
+  float ylo = 1.0e30f, yhi = -1.0e30f;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        if (fx[k] >= sl && fx[k] <= sr) { ylo = fminf(ylo, fy[k]); yhi = fmaxf(yhi, fy[k]); }
-        const int n = (k + 1) % 3;
-        const float dxe = fx[n] - fx[k], dye = fy[n] - fy[k];
-        // 1/dxe: hardware reciprocal + one Newton step (<= ~1 ulp; the
-        // widening below covers it), instead of two IEEE divisions per edge
-        const float r0 = __builtin_amdgcn_rcpf(dxe);
-        const float rdx = fmaf(fmaf(-dxe, r0, 1.0f), r0, r0);
+  for (int k = 0; k < 3; ++k) {
+    if (fx[k] >= sl && fx[k] <= sr) { ylo = fminf(ylo, fy[k]); yhi = fmaxf(yhi, fy[k]); }
+    const int n = (k + 1) % 3;
+    const float dxe = fx[n] - fx[k], dye = fy[n] - fy[k];
+    // 1/dxe: hardware reciprocal + one Newton step (<= ~1 ulp; the half-pixel
+    // widening below covers it), instead of two IEEE divisions per edge
+    const float r0 = __builtin_amdgcn_rcpf(dxe);
+    const float rdx = fmaf(fmaf(-dxe, r0, 1.0f), r0, r0);
 #pragma unroll
-        for (int side = 0; side < 2; ++side) {
-          const float xs = side ? sr : sl;
-          if ((fx[k] - xs) * (fx[n] - xs) < 0.0f) {
-            const float yc = fy[k] + (xs - fx[k]) * rdx * dye;
-            ylo = fminf(ylo, yc);
-            yhi = fmaxf(yhi, yc);
-          }
-        }
+    for (int side = 0; side < 2; ++side) {
+      const float xs = side ? sr : sl;
+      if ((fx[k] - xs) * (fx[n] - xs) < 0.0f) {
+        const float yc = fy[k] + (xs - fx[k]) * rdx * dye;
+        ylo = fminf(ylo, yc);
+        yhi = fmaxf(yhi, yc);
       }
-      if (ylo <= yhi) {
-        bool small = true;
+    }
+  }
+  if (!(ylo <= yhi)) return 0u;
+  bool small = true;
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-          small &= abs(X[k] - ox * 256) < (1 << 14) && abs(Y[k] - oy * 256) < (1 << 14);
+  for (int k = 0; k < 3; ++k)
+    small &= abs(X[k] - ox * 256) < (1 << 14) && abs(Y[k] - oy * 256) < (1 << 14);
 #if CSG_TIGHT_ROWS
-        // Vertices within 64 px of the tile: every value above is below 2^16
-        // units and off by < 0.01 units, so a 1/16-px widening suffices (half
-        // a pixel otherwise added about one empty row per record and tile).
-        const float wid = small ? 16.0f : 128.0f;
+  // Vertices within 64 px of the tile: every value above is below 2^16 units
+  // and off by < 0.01 units, so a 1/16-px widening suffices (half a pixel
+  // otherwise added about one empty row per record and tile).
+  const float wid = small ? 16.0f : 128.0f;
 #else
-        const float wid = 128.0f;
+  const float wid = 128.0f;
 #endif
-        const int r0 = (int)ceilf((ylo - 128.0f - wid) * (1.0f / 256.0f));
-        const int r1 = (int)floorf((yhi - 128.0f + wid) * (1.0f / 256.0f));
-        y0 = max(y0, oy + r0);
-        y1 = min(y1, oy + r1);
-        cls = small ? 1u : 2u;
-        row0 = (uint32_t)(y0 - oy) | (small ? 0x80u : 0u);
-        rows = y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
-      }
-    }
-  }
-  // groups the bound does not read go to LDS now (fewer live registers below)
-  L.img.q[0][slot] = q[0];
-  L.img.q[1][slot] = q[1];
-  L.img.q[5][slot] = q[5];
-  uint32_t kb16 = 0;
-#if CSG_COARSE_Z
-  if (rows && bound) {
-    // invW is affine in the pixel position, so over the box x0..x1, y0..y1
-    // its exact value peaks at a corner.  The computed value at any pixel
-    // differs from the exact one by at most |invdet| * 5.1u * T + 1.01u *
-    // inv_near (u = 2^-24, T = sum |A_k| x + |B_k| y + |C_k| at the box's far
-    // corner, for fragments inside the depth range); err doubles that margin
-    // twice over.  A NaN or infinite term disables the bound.
-    const float A[3] = {f_(q[2].z), f_(q[2].w), f_(q[3].x)}, B[3] = {f_(q[3].y), f_(q[3].z), f_(q[3].w)};
-    const float C[3] = {f_(q[4].x), f_(q[4].y), f_(q[4].z)};
-    const float idet = f_(q[4].w);
-    float e[3], ss, w00, w10, w01, w11;
-    hom_eval(A, B, C, idet, x0, y0, e, ss, w00);
-    hom_eval(A, B, C, idet, x1, y0, e, ss, w10);
-    hom_eval(A, B, C, idet, x0, y1, e, ss, w01);
-    hom_eval(A, B, C, idet, x1, y1, e, ss, w11);
-    const float Xf = (float)x1 + 0.5f, Yf = (float)y1 + 0.5f;
-    float T = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) T += (fabsf(A[k]) * Xf + fabsf(B[k]) * Yf) + fabsf(C[k]);
-    const float err = fabsf(idet) * T * 0x1p-20f + c.inv_near * 0x1p-22f;
-    const float mx = fmaxf(fmaxf(w00, w10), fmaxf(w01, w11));
-    const bool finite = w00 == w00 && w10 == w10 && w01 == w01 && w11 == w11 && err < INFINITY;
-    const float bnd = mx + 2.0f * err;
-    if (finite) {
-      if (bnd < c.inv_far) {
-        rows = 0;                                     // every fragment fails the depth range
-      } else {
-        kb16 = (0xFFFFFFFFu - fbits(fminf(bnd, c.inv_near))) >> 16;
-        if (segs_behind(L.segs, y0 - oy, y1 - oy, x0 - ox, x1 - ox, kb16)) rows = 0;
-      }
-      if (!rows && (DBG(c.dbg) & 512u)) atomicAdd(&c.ctr[9], 1u);   // profiling: records culled
-    }
-  }
-#endif
-  q[6].w = (q[6].w & 0xFFu) | (kb16 << 16);
-  L.img.q[2][slot] = q[2];
-  L.img.q[3][slot] = q[3];
-  L.img.q[4][slot] = q[4];
-  L.img.q[6][slot] = q[6];
-  return rows;
+  const int r0 = (int)ceilf((ylo - 128.0f - wid) * (1.0f / 256.0f));
+  const int r1 = (int)floorf((yhi - 128.0f + wid) * (1.0f / 256.0f));
+  y0 = max(y0, oy + r0);
+  y1 = min(y1, oy + r1);
+  row0 = (uint32_t)(y0 - oy) | (small ? 0x80u : 0u);
+  return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
 
-// Three exclusive scans over the 256-thread block sharing one barrier pair;
-// `wsum` is LDS[12].
-__device__ __forceinline__ void block_excl_scan3(const uint32_t (&v)[3], uint32_t* wsum, uint32_t (&ex)[3],
-                                                 uint32_t (&tot)[3]) {
-  uint32_t inc[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) inc[q] = wave_incl_scan(v[q]);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 63) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) wsum[4 * q + w] = inc[q];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    uint32_t off = 0, t = 0;
-#pragma unroll
-    for (int k = 0; k < kBlock / 64; ++k) {
-      const uint32_t x = wsum[4 * q + k];
-      off += (k < w) ? x : 0u;
-      t += x;
-    }
-    ex[q] = off + inc[q] - v[q];
-    tot[q] = t;
-  }
-  __syncthreads();
-}
+struct RasterLds {
+  RecImage img;                         // staged bin records
+#if CSG_L1_BITMAP
+  uint32_t starts1[kStage];             // bit i: a staged record's rows start at level-1 item i
+  uint16_t before1[kStage + 1];         // records starting before item 32*d
+  uint32_t crec[kStage];                // compact record: slot | first item << 8
+#else
+  uint32_t pre[kBlock + 1];             // row-item prefix per record
+#endif
+  uint8_t row0[kBlock];                 // first tile row of each staged record | 0x80 if small
+  uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
+#if CSG_L2_BITMAP
+  uint32_t starts[kBlock];              // bit i: a span starts at level-2 item i (<= 256 spans x 32 px)
+  uint16_t before[kBlock + 1];          // spans starting before item 32*d
+#else
+  uint32_t pre2[kBlock + 1];            // pixel-item prefix per span
+#endif
+  uint32_t wsum[kBlock / 64];
+};
 
 // Block-level two-level expansion of kStage-record batches.
 //   level 1: (record, row) items, one per thread -> exact row span
@@ -1167,101 +1027,64 @@ __device__ __forceinline__ void block_excl_scan3(const uint32_t (&v)[3], uint32_
 // An item finds its record / span by a rank query over a bitmap of starts
 // (measured: -5.5% k_raster vs a 4-ary search over the prefix; a per-item
 // owner map cost a workgroup per CU in LDS).
-// Level-1 items are ordered by record class -- exact-mask records, then
-// small, then large -- so a wave runs one span path, not all three.
-// Coarse z (CSG_COARSE_Z): from the second batch on, the segment maxima of
-// the z-buffer are refreshed; records whose nearest possible depth is behind
-// every pixel of their box are dropped at staging, rows behind their
-// segments in level 1.  Exact: a dropped fragment's key is larger than the
-// pixel's key at that time, and keys only decrease.
 __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds& L, uint32_t beg,
                                              uint32_t end, const uint32_t* bins, const Rec* recs) {
   const int tid = threadIdx.x;
   for (uint32_t base = beg; base < end; base += kStage) {
-    const bool later = CSG_COARSE_Z && base > beg;
-    if (later) {
-      refresh_segs(c.zb, L.segs);
-      __syncthreads();
-    }
-    uint32_t row0, cls;
-    const uint32_t rows = stage_record(c, recs, bins, base + tid, end, b.rec_cap, L, tid, later, row0, cls);
-    if (tid < kStage) L.row0[tid] = (uint8_t)row0;
+    uint32_t row0;
+    const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
+    L.row0[tid] = (uint8_t)row0;
     if ((DBG(b.dbg) & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
       atomicAdd(&b.overflow[1], 1u);
       atomicAdd(&b.overflow[2], rows);
-      if (cls == 0) atomicAdd(&b.overflow[11], rows);
     }
-    // records with rows get compact indices in class order; item -> record
-    // is a rank query over a bitmap of record starts (as for level 2 below)
+#if CSG_L1_BITMAP
+    // records with rows get compact indices; item -> record is a rank query
+    // over a bitmap of record starts (as for level 2 below)
     if (tid < kStage) L.starts1[tid] = 0u;   // ordered before the atomics by the scan's barriers
     if (tid == 0) L.before1[0] = 0;
-    const uint32_t one = rows ? (rows | 0x10000u) : 0u;   // items | records << 16
-#if CSG_CLASS_ORDER
-    const uint32_t v3[3] = {cls == 0 ? one : 0u, cls == 1 ? one : 0u, cls == 2 ? one : 0u};
-    uint32_t ex3[3], tot3[3];
-    block_excl_scan3(v3, L.wsum, ex3, tot3);
-    const uint32_t n0 = tot3[0] & 0xFFFFu, n1 = tot3[1] & 0xFFFFu;
-    const uint32_t tot1 = n0 + n1 + (tot3[2] & 0xFFFFu);
-#else
     uint32_t tot1p;
-    const uint32_t ex1p = block_excl_scan(one, L.wsum, tot1p);
+    const uint32_t ex1p = block_excl_scan(rows | (rows ? 0x10000u : 0u), L.wsum, tot1p);
     const uint32_t tot1 = tot1p & 0xFFFFu;
-#endif
     if (rows) {
-#if CSG_CLASS_ORDER
-      const uint32_t e = ex3[cls];
-      const uint32_t item0 = cls == 0 ? 0u : cls == 1 ? n0 : n0 + n1;
-      const uint32_t rec0 = cls == 0 ? 0u : cls == 1 ? (tot3[0] >> 16) : (tot3[0] >> 16) + (tot3[1] >> 16);
-      const uint32_t ex1 = item0 + (e & 0xFFFFu), ci = rec0 + (e >> 16), e_end = ex1 + rows;
-#else
       const uint32_t ex1 = ex1p & 0xFFFFu, ci = ex1p >> 16, e_end = ex1 + rows;
-#endif
       L.crec[ci] = (uint32_t)tid | (ex1 << 8);
       atomicOr(&L.starts1[ex1 >> 5], 1u << (ex1 & 31u));
       if ((e_end & ~31u) > ex1) L.before1[e_end >> 5] = (uint16_t)(ci + 1u);
     }
+#else
+    uint32_t tot1;
+    const uint32_t ex1 = block_excl_scan(rows, L.wsum, tot1);
+    L.pre[tid] = ex1;
+    if (tid == kBlock - 1) L.pre[kBlock] = ex1 + rows;
+#endif
     __syncthreads();
     for (uint32_t c1 = 0; c1 < ((DBG(b.dbg) & 256u) ? 0u : tot1); c1 += kBlock) {
-#if CSG_COARSE_Z >= 2
-      if (later && c1 > 0) refresh_segs(c.zb, L.segs);   // stale reads in this phase are safe
-#endif
       const uint32_t j1 = c1 + tid;
       uint32_t w2 = 0, sp = 0;
       int xl = 0;
       if (j1 < tot1) {
+#if CSG_L1_BITMAP
         const uint32_t w1 = L.starts1[j1 >> 5], nb1 = L.before1[j1 >> 5];
         const uint32_t cr = L.crec[nb1 + (uint32_t)__popc(w1 & (0xFFFFFFFFu >> (31u - (j1 & 31u)))) - 1u];
         const int k = (int)(cr & 255u);
         const uint32_t first = cr >> 8;
+#else
+        const int k = find_item(L.pre, j1);
+        const uint32_t first = L.pre[k];
+#endif
         const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
+        const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
+        const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
         const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTile - 1);
         const uint32_t r0b = L.row0[k];
         const int ly = (int)(r0b & 31u) + (int)(j1 - first);
         int xr;
-#if CSG_COARSE_Z >= 2
-        const uint32_t kb16 = later ? (L.img.q[6][k].w >> 16) : 0u;
-#else
-        constexpr uint32_t kb16 = 0u;
-#endif
-        if (kb16 && segs_behind(L.segs, ly, ly, x0, x1, kb16)) {   // the row is behind the z-buffer
-          xl = 1; xr = 0;
-          if (DBG(b.dbg) & 512u) atomicAdd(&b.overflow[10], 1u);
-        } else if (DBG(b.dbg) & 1024u) {    // ablation: no span computation
-          xl = 1; xr = 0;
-        } else if (g0.w == kMaskFlag) {     // the row's covered run straight from the mask
-          const uint32_t nib = (g0.x >> (4u * (uint32_t)(c.oy + ly - (int)(g1.z >> 16)))) & 15u;
-          const int m0 = (int)(g1.z & 0xFFFFu) - c.ox;   // tile column of mask bit 0
-          xl = max(m0 + __ffs(nib) - 1, x0);
-          xr = min(m0 + 31 - __clz(nib), x1);
-          if (!nib) { xl = 1; xr = 0; }
-        } else {
-          const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
-          const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
-          if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
-          else {
-            if (DBG(b.dbg) & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
-            row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
-          }
+        if (DBG(b.dbg) & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
+        else if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
+        else {
+          if (DBG(b.dbg) & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
+          row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
         }
         if (xl <= xr) {
           w2 = (uint32_t)(xr - xl + 1);
@@ -1272,6 +1095,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         atomicAdd(&b.overflow[3], 1u);
         atomicAdd(&b.overflow[4], w2);
       }
+#if CSG_L2_BITMAP
       // Non-empty spans get compact indices (one packed scan gives item
       // offset and index).  Item -> span is then a rank query: a bitmap of
       // span starts plus, per 32-item word, the spans starting before it (the
@@ -1296,6 +1120,19 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
+#else
+      uint32_t tot2;
+      const uint32_t ex2 = block_excl_scan(w2, L.wsum, tot2);
+      L.span[tid] = sp | ((ex2 - (uint32_t)xl + 32u) << 16);
+      L.pre2[tid] = ex2;
+      if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
+      __syncthreads();
+      for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kBlock) {
+        const uint32_t spj = L.span[find_item(L.pre2, j)];
+        fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
+      }
+      __syncthreads();
+#endif
     }
   }
 }
@@ -1452,10 +1289,8 @@ struct ResolveLds {
 // The resolve's LDS aliases the raster loop's in a union inside k_raster.
 // (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4;
 // 26,656 B keeps 6.)
-// LDS is allocated to a workgroup in 1,280-B granules (measured: 26,656 B kept
-// 6 workgroups per CU, 31,776 B 5 and 32,512 B only 4), so six need <= 26,880 B.
 static_assert((sizeof(RasterLds) > sizeof(ResolveLds) ? sizeof(RasterLds) : sizeof(ResolveLds)) + kTilePix * 8 <=
-                  (CSG_WAVES >= 7 ? 21760u : CSG_WAVES == 6 ? 26880u : CSG_WAVES == 5 ? 32000u : 40960u),
+                  (CSG_WAVES >= 7 ? 22528u : CSG_WAVES == 6 ? 26700u : CSG_WAVES == 5 ? 32256u : 40960u),
               "k_raster LDS must allow CSG_WAVES workgroups per CU");
 
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
@@ -1576,7 +1411,6 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     return;
   }
   for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
-  if (tid < kTile) L.r.segs[tid] = ~0ull;         // coarse z: nothing drawn yet
   const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
   RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow};
