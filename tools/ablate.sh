@@ -8,6 +8,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export CSG_LIB=${CSG_LIB:-$PWD/constructionsceneposeestimation_amd/libcsg_abl.so}
 for d in ${DBGS:-0 1 2 4 8 16 0}; do
-  CSG_DEBUG=$d timeout -k 10 200 python bench.py --cpu-sample 0 --steps 20 > gpurun_out/ablate_$d.json 2>/dev/null || exit 1
+  CSG_DEBUG=$d timeout -k 10 200 python bench.py --verify-frames 0 --steps 20 > gpurun_out/ablate_$d.json 2>/dev/null || exit 1
   python3 -c "import json; d=json.load(open('gpurun_out/ablate_$d.json')); print('CSG_DEBUG=$d', d['value'], d['stage_ms_per_step'])"
 done
