@@ -12,8 +12,9 @@ from typing import Optional
 PKG = os.path.dirname(os.path.abspath(__file__))
 # CSG_LIB names an alternative build of the same ABI (A/B timing of kernel variants)
 LIB_PATH = os.environ.get("CSG_LIB") or os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 6  # CSG_ABI_VERSION in include/csg_api.h
+ABI_VERSION = 7  # CSG_ABI_VERSION in include/csg_api.h
 KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
+COVERED_UNKNOWN = 0x80000000  # csg_outputs.label_covered flag: a tile held more than 32 labels
 
 EXPORTED = (
     "csg_create", "csg_destroy", "csg_last_error", "csg_abi_version", "csg_upload_scene",
@@ -65,7 +66,8 @@ class Outputs(C.Structure):
     _fields_ = [("rgb", C.c_void_p), ("instance", C.c_void_p), ("depth", C.c_void_p),
                 ("keypoints_uv", C.c_void_p), ("keypoints_vis", C.c_void_p), ("inst_stats", C.c_void_p),
                 ("n_labels", C.c_uint32), ("on_device", C.c_int32), ("normals", C.c_void_p),
-                ("points", C.c_void_p)]
+                ("points", C.c_void_p), ("depth_vis", C.c_void_p), ("depth_range", C.c_void_p),
+                ("label_covered", C.c_void_p)]
 
 
 class BatchStats(C.Structure):
@@ -81,6 +83,22 @@ class Timing(C.Structure):
 
 
 _lib: Optional[C.CDLL] = None
+
+
+def _share_hip_runtime() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm ships its own
+    libamdhip64.so (soname libamdhip64.so.7, the one libcsg.so needs): loaded
+    first, it also serves libcsg.so.  If libcsg.so came first, /opt/rocm's
+    copy would be loaded and a later ``import torch`` would load a second
+    runtime, whose GPU initialisation then fails ("No HIP GPUs are
+    available").  So when torch is installed it is imported before libcsg.so
+    (CSG_OWN_HIP_RUNTIME=1 skips this for processes that never use torch)."""
+    import sys
+    if "torch" in sys.modules or os.environ.get("CSG_OWN_HIP_RUNTIME") == "1":
+        return
+    import importlib.util
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:
@@ -99,6 +117,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
                 raise CsgError(f"libcsg.so missing and could not be built: {e}") from e
     if not os.path.exists(path):
         raise CsgError(f"libcsg.so not found at {path}; run python -m constructionsceneposeestimation_amd.build")
+    _share_hip_runtime()
     lib = C.CDLL(path)
     vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int32
     lib.csg_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]

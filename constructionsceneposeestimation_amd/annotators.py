@@ -9,7 +9,8 @@ build's additions.
   "idToSemantics"}}`` (:1818-1842); id 0 = background/unlabelled, id k+1 =
   object ``inst_idx`` k;
 * ``bounding_box_3d`` -> ``{"data": structured records (semanticId, x/y/z
-  min/max, 4x4 transform, occlusionRatio), "info": {"primPaths",
+  min/max, 4x4 transform, occlusionRatio = 1 - visible / unoccluded pixels
+  from the GPU's label coverage), "info": {"primPaths",
   "worldBounds"}}`` for the objects visible in the frame (:1780-1790,
   :1916-1922, read positionally by ``bboxDict_to_transform`` :562-564);
   ``worldBounds`` (N,2,3) is the world AABB of each object's vertices,
@@ -34,7 +35,7 @@ from .labels import bbox3d_records
 SUPPORTED = ("rgb", "distance_to_image_plane", "instance_segmentation", "bounding_box_3d",
              "bounding_box_2d_tight", "pointcloud", "keypoints_2d", "normals")
 # renderer outputs an annotator needs beyond the camera's defaults
-_NEEDS = {"pointcloud": ("points",), "normals": ("normals",)}
+_NEEDS = {"pointcloud": ("points",), "normals": ("normals",), "bounding_box_3d": ("covered",)}
 
 
 def unproject_depth(depth: np.ndarray, cam_to_world: np.ndarray, intr) -> np.ndarray:
@@ -88,7 +89,7 @@ class Annotator:
             stats = out["inst_stats"]
             vis = [j for j, o in enumerate(scene.objects) if o.inst_idx < stats.shape[0] and stats[o.inst_idx, 0] > 0]
             if self.name == "bounding_box_3d":
-                recs = bbox3d_records(scene, cam.stage.state.object_frames)
+                recs = bbox3d_records(scene, cam.stage.state.object_frames, stats, out.get("label_covered"))
                 return {"data": recs[vis], "info": {"primPaths": [scene.objects[j].prim_path for j in vis],
                                                      "idToLabels": {j: scene.objects[j].class_name for j in vis},
                                                      "worldBounds": cam.object_world_bounds()[vis]}}

@@ -132,6 +132,11 @@ struct csg_ctx {
   DevBuf<int32_t> o_kp_vis;
   DevBuf<uint32_t> kp_pix, kp_tiles;
   DevBuf<uint32_t> o_stats;
+  DevBuf<uint8_t> o_dvis;               // depth visualisation (host-output mode)
+  DevBuf<float> o_drange;
+  DevBuf<uint32_t> o_cov;               // label coverage (host-output mode)
+  DevBuf<uint32_t> drange;              // [2][chain frames] min / max depth bits (k_depth_range)
+  DevBuf<uint32_t> jet;                 // JET colour map, 256 x (r | g << 8 | b << 16)
 
   // timing: ring of per-batch event quintuples (recorded, never waited on in the loop)
   bool timing = true;
@@ -196,6 +201,30 @@ static int take_flags(csg_ctx* c, uint32_t* flags_out) {
                  c->rec_cap, c->bin_cap);
 }
 
+// OpenCV's COLORMAP_JET (the reference's cv2.applyColorMap, GDP:1703): the
+// GNU Octave "jet" map sampled at x = k/255, stored as float, scaled by 255
+// in float and rounded half to even (Mat::convertTo to CV_8U).  OpenCV is not
+// in this image, so the table is a restatement, not a copy.
+static void jet_lut(uint32_t* lut) {
+  for (int k = 0; k < 256; ++k) {
+    const double x = (double)k / 255.0;
+    const double r = (x >= 3.0 / 8 && x < 5.0 / 8) ? 4 * x - 1.5 : (x >= 5.0 / 8 && x < 7.0 / 8) ? 1.0
+                     : (x >= 7.0 / 8) ? -4 * x + 4.5 : 0.0;
+    const double g = (x >= 1.0 / 8 && x < 3.0 / 8) ? 4 * x - 0.5 : (x >= 3.0 / 8 && x < 5.0 / 8) ? 1.0
+                     : (x >= 5.0 / 8 && x < 7.0 / 8) ? -4 * x + 3.5 : 0.0;
+    const double b = (x < 1.0 / 8) ? 4 * x + 0.5 : (x >= 1.0 / 8 && x < 3.0 / 8) ? 1.0
+                     : (x >= 3.0 / 8 && x < 5.0 / 8) ? -4 * x + 2.5 : 0.0;
+    const double ch[3] = {r, g, b};
+    uint32_t v = 0;
+    for (int c = 0; c < 3; ++c) {
+      const float p = (float)ch[c] * 255.0f;
+      const long q = std::lrint(p);   // default rounding mode: nearest, ties to even
+      v |= (uint32_t)std::min(255L, std::max(0L, q)) << (8 * c);
+    }
+    lut[k] = v;
+  }
+}
+
 extern "C" {
 
 int csg_abi_version(void) { return CSG_ABI_VERSION; }
@@ -230,6 +259,12 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   // csg_render_batch has read it
   if (e == hipSuccess) e = c->overflow.alloc(16);
   if (e == hipSuccess) e = hipMemset(c->overflow.p, 0, 16 * sizeof(uint32_t));
+  if (e == hipSuccess) e = c->jet.alloc(256);
+  if (e == hipSuccess) {
+    uint32_t lut[256];
+    jet_lut(lut);
+    e = hipMemcpy(c->jet.p, lut, sizeof(lut), hipMemcpyHostToDevice);
+  }
   c->ev = c->ring.data();
   if (e != hipSuccess) {
     c->err = hipGetErrorString(e);
@@ -255,6 +290,7 @@ void csg_destroy(csg_ctx* c) {
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
   c->kp_w.release(); c->kp_pix.release(); c->kp_tiles.release();
   c->o_points.release(); c->o_normals.release(); c->cam.release(); c->fset.release();
+  c->o_dvis.release(); c->o_drange.release(); c->o_cov.release(); c->drange.release(); c->jet.release();
   for (uint32_t k = 0; k < csg_ctx::kStaging; ++k) {
     if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
     if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);
@@ -716,6 +752,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     b.normals = out->normals;
     b.points = out->points;
     b.stats = out->inst_stats;
+    b.covered = out->label_covered;
     b.kp_uv = out->keypoints_uv;
     b.kp_vis = out->keypoints_vis;
   } else {
@@ -728,8 +765,33 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       HIP_TRY(c, c->o_stats.alloc((size_t)F * out->n_labels * 5));
       b.stats = c->o_stats.p;
     }
+    if (out->label_covered && out->n_labels) {
+      HIP_TRY(c, c->o_cov.alloc((size_t)F * out->n_labels));
+      b.covered = c->o_cov.p;
+    }
   }
   if (!out->inst_stats) b.stats = nullptr;
+  if (!out->label_covered || !out->n_labels) b.covered = nullptr;
+  // depth visualisation: needs the depth image (internal scratch when the
+  // caller did not ask for depth itself)
+  const bool want_dvis = out->depth_vis || out->depth_range;
+  uint8_t* dvis = nullptr;
+  float* drange_out = nullptr;
+  if (want_dvis) {
+    if (!b.depth) {
+      HIP_TRY(c, c->o_depth.alloc(F * npx));
+      b.depth = c->o_depth.p;
+    }
+    HIP_TRY(c, c->drange.alloc((size_t)2 * c->chain_frames));
+    if (out->depth_vis) {
+      if (dev) dvis = out->depth_vis;
+      else { HIP_TRY(c, c->o_dvis.alloc(F * npx * 3)); dvis = c->o_dvis.p; }
+    }
+    if (out->depth_range) {
+      if (dev) drange_out = out->depth_range;
+      else { HIP_TRY(c, c->o_drange.alloc((size_t)F * 2)); drange_out = c->o_drange.p; }
+    }
+  }
   b.tile_words = (c->n_tiles + 31u) / 32u;
   if (want_kp) {
     HIP_TRY(c, c->kp_w.alloc((size_t)c->chain_frames * c->n_kp));
@@ -755,6 +817,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (bc.normals) bc.normals += (size_t)c0 * npx * 3;
     if (bc.points) bc.points += (size_t)c0 * npx * 3;
     if (bc.stats) bc.stats += (size_t)c0 * b.n_labels * 5;
+    if (bc.covered) bc.covered += (size_t)c0 * b.n_labels;
     if (want_kp) {
       bc.kp_uv += (size_t)c0 * c->n_kp * 2;
       bc.kp_vis += (size_t)c0 * c->n_kp;
@@ -764,6 +827,11 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
     if (want_kp) HIP_TRY(c, hipMemsetAsync(bc.kp_tiles, 0, sizeof(uint32_t) * Fc * bc.tile_words, st));
     launch_init_stats(bc, Fc, st);
+    if (bc.covered) HIP_TRY(c, hipMemsetAsync(bc.covered, 0, sizeof(uint32_t) * Fc * b.n_labels, st));
+    if (want_dvis) {   // row 0: min (all ones), row 1: max (zero)
+      HIP_TRY(c, hipMemsetAsync(c->drange.p, 0xFF, sizeof(uint32_t) * Fc, st));
+      HIP_TRY(c, hipMemsetAsync(c->drange.p + Fc, 0, sizeof(uint32_t) * Fc, st));
+    }
     if (c->timing) {
       const uint32_t slot = (uint32_t)(c->ring_count % csg_ctx::kRing);
       c->ev = &c->ring[(size_t)slot * 5];
@@ -782,6 +850,14 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
     launch_raster(s, bc, Fc, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
+    if (want_dvis) {
+      launch_depth_range(bc.depth, (uint32_t)npx, Fc, c->drange.p, st);
+      if (dvis || drange_out) {
+        uint8_t* vo = dvis ? dvis + (size_t)c0 * npx * 3 : nullptr;
+        float* ro = drange_out ? drange_out + (size_t)c0 * 2 : nullptr;
+        launch_depth_vis(bc.depth, (uint32_t)npx, Fc, c->drange.p, c->jet.p, vo, ro, st);
+      }
+    }
     c->last_F = Fc;
   }
   HIP_TRY(c, hipGetLastError());
@@ -793,6 +869,10 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (out->points) HIP_TRY(c, hipMemcpyAsync(out->points, b.points, F * npx * 12, hipMemcpyDeviceToHost, st));
     if (b.stats)
       HIP_TRY(c, hipMemcpyAsync(out->inst_stats, b.stats, (size_t)F * out->n_labels * 5 * 4, hipMemcpyDeviceToHost, st));
+    if (b.covered)
+      HIP_TRY(c, hipMemcpyAsync(out->label_covered, b.covered, (size_t)F * out->n_labels * 4, hipMemcpyDeviceToHost, st));
+    if (dvis) HIP_TRY(c, hipMemcpyAsync(out->depth_vis, dvis, F * npx * 3, hipMemcpyDeviceToHost, st));
+    if (drange_out) HIP_TRY(c, hipMemcpyAsync(out->depth_range, drange_out, (size_t)F * 8, hipMemcpyDeviceToHost, st));
     if (want_kp && out->keypoints_uv)
       HIP_TRY(c, hipMemcpyAsync(out->keypoints_uv, b.kp_uv, (size_t)F * c->n_kp * 8, hipMemcpyDeviceToHost, st));
     if (want_kp && out->keypoints_vis)

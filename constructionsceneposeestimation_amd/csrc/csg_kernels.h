@@ -13,6 +13,8 @@ constexpr uint32_t kUidShift = 20;        // uid = (instance << 20) | triangle
 constexpr uint32_t kMaxInstances = 1u << (32 - kUidShift);
 constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
 constexpr int kMaxLdsLabels = 256;        // per-label pixel stats kept in LDS
+constexpr int kCovSlots = 32;             // labels per tile in k_raster's coverage table (occlusion)
+constexpr uint32_t kCovUnknown = 0x80000000u;   // covered[] flag: a tile held more than kCovSlots labels
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
 constexpr uint32_t kNoAlpha = 0xFFFFFFFFu;  // Rec::atex of a record without alpha test
 constexpr uint32_t kCamFloats = 16;         // per-frame unprojection constants (frame_camera)
@@ -111,6 +113,7 @@ struct BatchDev {
   float* points;               // [F][H][W][3] world xyz (NaN: no hit) or null
   float* cam;                  // [F][kCamFloats] camera-to-world rotation, position, fx fy cx cy
   uint32_t* stats;             // [F][n_labels][5] or null
+  uint32_t* covered;           // [F][n_labels] unoccluded pixels per label (k_raster<true> only), bit 31: unknown
   uint32_t n_labels;
   const float* kp;             // [n_sets][K][3]
   uint32_t n_kp;
@@ -131,6 +134,12 @@ void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blo
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+// depth visualisation (GDP:1690-1709): per-frame min / max of the valid depth
+// (range [2][F] as float bits: row 0 min, initialised to ~0; row 1 max, to 0),
+// then the JET-coloured RGB8 image; lut = 256 packed r | g << 8 | b << 16
+void launch_depth_range(const float* depth, uint32_t npx, uint32_t F, uint32_t* range, hipStream_t st);
+void launch_depth_vis(const float* depth, uint32_t npx, uint32_t F, const uint32_t* range, const uint32_t* lut,
+                      uint8_t* vis, float* range_out, hipStream_t st);
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_keypoints(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_inst_bounds(const SceneDev& s, const Chunk* chunks, uint32_t n_chunks, const float* models,

@@ -28,6 +28,8 @@
 // memory for instructions wherever the result is unchanged.
 #include <math.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "csg_kernels.h"
@@ -842,16 +844,6 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // ---------------------------------------------------------------------------
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
-struct RasterCtx {
-  const uint32_t* aquad;
-  const uint32_t* acls;
-  unsigned long long* zb;
-  int ox, oy;
-  float inv_near, inv_far;
-  uint32_t dbg;
-  uint32_t* ctr;   // profiling counters (CSG_DEBUG 512 only)
-};
-
 // LDS image of up to kStage staged records as seven 16-B field groups (the Rec
 // layout cut at 16-B boundaries), group-major: lanes reading one group of
 // different records hit consecutive 16-B slots (no bank conflicts; a Rec-
@@ -884,7 +876,7 @@ struct RasterCtx {
 #define CSG_WAVES 6             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
 #endif
 #if CSG_WAVES > 0
-#define CSG_RASTER_ATTR __attribute__((amdgpu_waves_per_eu(CSG_WAVES, CSG_WAVES)))
+#define CSG_RASTER_ATTR __attribute__((amdgpu_waves_per_eu(kCov ? 5 : CSG_WAVES, kCov ? 5 : CSG_WAVES)))
 #else
 #define CSG_RASTER_ATTR
 #endif
@@ -894,11 +886,58 @@ struct RecImage {
   uint4 q[kRecGroups][kStage];
 };
 
+// Coverage table of k_raster<true> (occlusion, GDP:1780-1790 occlusionRatio):
+// for each label seen in the tile, the pixels some fragment of it covers
+// (covered centre, depth in range, alpha test passed; no depth test), as a
+// 32x32 bit image.  A label that finds no slot (more than kCovSlots labels in
+// one tile) marks the tile: its labels are then flagged unknown and their
+// counts are not added, so the result does not depend on fragment order.
+struct CovLds {
+  int32_t rlabel[kStage];               // label of each staged record (-1: not counted)
+  uint32_t keys[kCovSlots];             // label of each slot (kNoAlpha: empty)
+  uint32_t mask[kCovSlots][kTile];      // per slot: bit lx of word ly
+  uint32_t ovf;                         // some label found no slot
+};
+
+struct RasterCtx {
+  const uint32_t* aquad;
+  const uint32_t* acls;
+  unsigned long long* zb;
+  int ox, oy;
+  float inv_near, inv_far;
+  uint32_t dbg;
+  uint32_t* ctr;   // profiling counters (CSG_DEBUG 512 only)
+  CovLds* cov;     // k_raster<true> only
+  uint32_t* gcov;  // covered[f][.] of this frame (k_raster<true> only)
+};
+
+// Mark pixel (lx, ly) covered by `label` in the tile's coverage table.
+__device__ __forceinline__ void cov_mark(const RasterCtx& c, uint32_t label, int lx, int ly) {
+  CovLds& t = *c.cov;
+  const uint32_t h = label & (uint32_t)(kCovSlots - 1);
+#pragma clang loop vectorize(disable) unroll(disable)
+  for (uint32_t p = 0; p < (uint32_t)kCovSlots; ++p) {
+    const uint32_t idx = (h + p) & (uint32_t)(kCovSlots - 1);
+    uint32_t cur = t.keys[idx];
+    if (cur == kNoAlpha) cur = atomicCAS(&t.keys[idx], kNoAlpha, label);
+    if (cur == kNoAlpha || cur == label) {
+      atomicOr(&t.mask[idx][ly], 1u << lx);
+      return;
+    }
+  }
+  t.ovf = 1u;
+  atomicOr(&c.gcov[label], kCovUnknown);
+}
+
+
 __device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
 
 // One fragment of staged record k at tile pixel (lx, ly), already known to be
 // covered: homogeneous depth, depth range, early-z against the LDS key,
 // alpha test (texture described inline in the record), then ds_min_u64.
+// With kCov (occlusion) every fragment in the depth range is alpha-tested,
+// early-z or not, and a surviving one marks its label's coverage bit.
+template <bool kCov>
 __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, int k, int lx, int ly) {
   const int px = c.ox + lx, py = c.oy + ly;
   const uint4 g2 = I.q[2][k], g3 = I.q[3][k], g4 = I.q[4][k];
@@ -909,6 +948,19 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
+  if constexpr (kCov) {
+    if (g2.y != kNoAlpha) {
+      const uint4 g5 = I.q[5][k], g6 = I.q[6][k];
+      const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
+      float u, v;
+      interp_uv(e, ssum, uv, u, v);
+      if (!alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)g6.w, u, v)) return;
+    }
+    const int32_t lab = c.cov->rlabel[k];
+    if (lab >= 0) cov_mark(c, (uint32_t)lab, lx, ly);
+    atomicMin(z, key);
+    return;
+  }
 #if CSG_OPAQUE_DIRECT
   // Without an alpha test the ds_min_u64 is the depth test: no early-z read,
   // compare and branch (a losing key leaves the word unchanged).
@@ -1027,13 +1079,24 @@ struct RasterLds {
 // An item finds its record / span by a rank query over a bitmap of starts
 // (measured: -5.5% k_raster vs a 4-ary search over the prefix; a per-item
 // owner map cost a workgroup per CU in LDS).
-__device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev& b, RasterLds& L, uint32_t beg,
-                                             uint32_t end, const uint32_t* bins, const Rec* recs) {
+template <bool kCov>
+__device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev& s, const BatchDev& b, RasterLds& L,
+                                             uint32_t beg, uint32_t end, const uint32_t* bins, const Rec* recs) {
   const int tid = threadIdx.x;
   for (uint32_t base = beg; base < end; base += kStage) {
     uint32_t row0;
     const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
     L.row0[tid] = (uint8_t)row0;
+    if constexpr (kCov) {   // label of the staged record (read back from this thread's own slot)
+      if (tid < kStage) {
+        int32_t lab = -1;
+        if (rows) {
+          lab = s.inst[L.img.q[2][tid].x >> kUidShift].label;
+          if (lab >= 0 && (uint32_t)lab >= b.n_labels) lab = -1;
+        }
+        c.cov->rlabel[tid] = lab;
+      }
+    }
     if ((DBG(b.dbg) & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
       atomicAdd(&b.overflow[1], 1u);
       atomicAdd(&b.overflow[2], rows);
@@ -1117,7 +1180,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
         const uint32_t w = L.starts[j >> 5], nb = L.before[j >> 5];
         const uint32_t rank = nb + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31u - (j & 31u))));
         const uint32_t spj = L.span[rank - 1u];
-        fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
+        fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
 #else
@@ -1129,7 +1192,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const BatchDev&
       __syncthreads();
       for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kBlock) {
         const uint32_t spj = L.span[find_item(L.pre2, j)];
-        fragment(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
+        fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
 #endif
@@ -1382,8 +1445,13 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
   }
 }
 
+// kCov: also the per-label coverage for occlusion (b.covered); a separate
+// instantiation (4.7 KiB more LDS: 5 workgroups per CU), launched only when
+// the caller asks for it.
+template <bool kCov>
 __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, BatchDev b) {
   __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
+  __shared__ CovLds covl;                            // kCov only (unreferenced otherwise: not allocated)
 #ifdef CSG_LDS_PAD
   __shared__ volatile uint32_t ldspad[CSG_LDS_PAD / 4];   // A/B only: occupancy probe
   if (b.dbg == 0xDEADu) ldspad[threadIdx.x] = 1u;
@@ -1411,12 +1479,35 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     return;
   }
   for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
+  if constexpr (kCov) {
+    for (int p = tid; p < kCovSlots * kTile; p += kBlock) (&covl.mask[0][0])[p] = 0u;
+    if (tid < kCovSlots) covl.keys[tid] = kNoAlpha;
+    if (tid == 0) covl.ovf = 0u;
+  }
   const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
-  RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow};
+  RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow, &covl,
+              kCov ? b.covered + (size_t)f * b.n_labels : nullptr};
   __syncthreads();
-  raster_block(c, b, L.r, beg, end, bins, recs);
+  raster_block<kCov>(c, s, b, L.r, beg, end, bins, recs);
   __syncthreads();
+  if constexpr (kCov) {
+    // per slot: popcount of its 32 mask words, 8 threads per slot (4 words
+    // each, lanes t..t+7 of one wave); the table is read-only from here on
+    static_assert(kCovSlots * 8 == kBlock && kTile == 32, "8 threads x 4 words per slot");
+    const uint32_t sl = (uint32_t)tid >> 3, w0 = ((uint32_t)tid & 7u) * 4u;
+    uint32_t n = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) n += (uint32_t)__popc(covl.mask[sl][w0 + w]);
+    n += (uint32_t)__shfl_xor((int)n, 1, 64);
+    n += (uint32_t)__shfl_xor((int)n, 2, 64);
+    n += (uint32_t)__shfl_xor((int)n, 4, 64);
+    const uint32_t lab = covl.keys[sl];
+    if ((tid & 7) == 0 && lab != kNoAlpha) {
+      if (covl.ovf) atomicOr(&c.gcov[lab], kCovUnknown);
+      else atomicAdd(&c.gcov[lab], n);
+    }
+  }
 
   if (DBG(b.dbg) & 1u) {   // ablation: keep the raster loop alive, skip the resolve
     if (tid == 0 && zb[0] == 0ull && b.inst) b.inst[0] = 0;
@@ -1774,6 +1865,110 @@ __global__ void k_project(const float* pts, uint32_t n, const float* pv, float W
 }
 
 // ---------------------------------------------------------------------------
+// Depth visualisation (GDP:1690-1709): the reference normalises the valid
+// depth (finite, > 0) of each frame by its min / max and maps it through
+// OpenCV's JET colour map.  Two streaming passes over the depth image
+// (HBM-bound): a per-frame min / max reduction, then the colour lookup.
+// Valid depths are positive floats, so their bit patterns order like the
+// values and the reduction runs on u32 atomics.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool depth_valid(float d) { return d > 0.0f && d < INFINITY; }
+
+template <bool kVec>
+__global__ __launch_bounds__(256) void k_depth_range(const float* __restrict__ depth, uint32_t npx,
+                                                     uint32_t* __restrict__ range, uint32_t F) {
+  const uint32_t f = blockIdx.y;
+  const float* d = depth + (size_t)f * npx;
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  auto take = [&](float v) {
+    if (depth_valid(v)) {
+      mn = min(mn, __float_as_uint(v));
+      mx = max(mx, __float_as_uint(v));
+    }
+  };
+  const uint32_t stride = gridDim.x * blockDim.x;
+  if constexpr (kVec) {   // npx % 4 == 0 and a 16-B aligned base: every frame starts aligned
+    const float4* d4 = reinterpret_cast<const float4*>(d);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npx / 4u; i += stride) {
+      const float4 v = d4[i];
+      take(v.x); take(v.y); take(v.z); take(v.w);
+    }
+  } else {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += stride) take(d[i]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+  }
+  __shared__ uint32_t wmn[4], wmx[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { wmn[w] = mn; wmx[w] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; ++k) { mn = min(mn, wmn[k]); mx = max(mx, wmx[k]); }
+    if (mn != 0xFFFFFFFFu) {
+      atomicMin(&range[f], mn);
+      atomicMax(&range[F + f], mx);
+    }
+  }
+}
+
+// Index of one depth value (GDP:1698-1700, NumPy 1.x promotion as Isaac Sim
+// runs it): (depth_max - depth_min) is a float32 scalar, + 1e-6 promotes it to
+// float64, and dividing the float32 array by that scalar casts it back to
+// float32; then ((d - min) / den) * 255 in float32 and astype(uint8) truncates.
+__device__ __forceinline__ uint32_t depth_index(float v, float mn, float den) {
+  if (!depth_valid(v)) return 0u;
+  const int q = (int)(((v - mn) / den) * 255.0f);
+  return (uint32_t)min(max(q, 0), 255);
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(256) void k_depth_vis(const float* __restrict__ depth, uint32_t npx, uint32_t F,
+                                                   const uint32_t* __restrict__ range, const uint32_t* __restrict__ lut,
+                                                   uint8_t* __restrict__ vis, float* __restrict__ range_out) {
+  __shared__ uint32_t tab[256];
+  const uint32_t f = blockIdx.y;
+  tab[threadIdx.x] = lut[threadIdx.x];
+  const uint32_t mnb = range[f], mxb = range[F + f];
+  const bool any = mnb != 0xFFFFFFFFu;          // no valid depth: the reference writes a black image
+  const float mn = __uint_as_float(mnb), mx = __uint_as_float(mxb);
+  const float den = (float)((double)(mx - mn) + 1e-6);
+  if (range_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    range_out[2 * f] = any ? mn : __builtin_nanf("");
+    range_out[2 * f + 1] = any ? mx : __builtin_nanf("");
+  }
+  __syncthreads();
+  if (!vis) return;       // range only
+  const size_t base = (size_t)f * npx;
+  if constexpr (kVec) {   // 4 pixels per thread: one float4 in, three dwords out
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= npx / 4u) return;
+    const float4 v = reinterpret_cast<const float4*>(depth + base)[q];
+    uint32_t c[4] = {0u, 0u, 0u, 0u};
+    if (any) {
+      c[0] = tab[depth_index(v.x, mn, den)];
+      c[1] = tab[depth_index(v.y, mn, den)];
+      c[2] = tab[depth_index(v.z, mn, den)];
+      c[3] = tab[depth_index(v.w, mn, den)];
+    }
+    uint32_t* o = reinterpret_cast<uint32_t*>(vis + (base + 4u * (size_t)q) * 3);
+    o[0] = c[0] | (c[1] << 24);
+    o[1] = (c[1] >> 8) | (c[2] << 16);
+    o[2] = (c[2] >> 16) | (c[3] << 8);
+  } else {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npx) return;
+    const uint32_t c = any ? tab[depth_index(depth[base + i], mn, den)] : 0u;
+    uint8_t* o = vis + (base + i) * 3;
+    o[0] = (uint8_t)(c & 255u);
+    o[1] = (uint8_t)((c >> 8) & 255u);
+    o[2] = (uint8_t)((c >> 16) & 255u);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
@@ -1811,7 +2006,8 @@ void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t
 #else
   dim3 g(s.n_tiles, F);
 #endif
-  hipLaunchKernelGGL(k_raster, g, dim3(kBlock), 0, st, s, b);
+  if (b.covered) hipLaunchKernelGGL(k_raster<true>, g, dim3(kBlock), 0, st, s, b);
+  else hipLaunchKernelGGL(k_raster<false>, g, dim3(kBlock), 0, st, s, b);
 }
 
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st) {
@@ -1834,6 +2030,24 @@ void launch_inst_bounds(const SceneDev& s, const Chunk* chunks, uint32_t n_chunk
 void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip, float* uv,
                     int32_t* vis, hipStream_t st) {
   hipLaunchKernelGGL(k_project, dim3((n + 255) / 256), dim3(256), 0, st, pts, n, pv12, W, H, near_clip, uv, vis);
+}
+
+void launch_depth_range(const float* depth, uint32_t npx, uint32_t F, uint32_t* range, hipStream_t st) {
+  const bool vec = (npx % 4u) == 0 && ((uintptr_t)depth & 15u) == 0;
+  const uint32_t per = vec ? npx / 4u : npx;
+  const uint32_t blocks = std::min<uint32_t>(64u, (per + 4095u) / 4096u);   // ~16 items per thread at 1080p
+  dim3 g(blocks ? blocks : 1u, F);
+  if (vec) hipLaunchKernelGGL(k_depth_range<true>, g, dim3(256), 0, st, depth, npx, range, F);
+  else hipLaunchKernelGGL(k_depth_range<false>, g, dim3(256), 0, st, depth, npx, range, F);
+}
+
+void launch_depth_vis(const float* depth, uint32_t npx, uint32_t F, const uint32_t* range, const uint32_t* lut,
+                      uint8_t* vis, float* range_out, hipStream_t st) {
+  const bool vec = (npx % 4u) == 0 && ((uintptr_t)depth & 15u) == 0 && ((uintptr_t)vis & 3u) == 0;
+  const uint32_t items = vec ? npx / 4u : npx;
+  dim3 g(vis ? (items + 255u) / 256u : 1u, F);
+  if (vec) hipLaunchKernelGGL(k_depth_vis<true>, g, dim3(256), 0, st, depth, npx, F, range, lut, vis, range_out);
+  else hipLaunchKernelGGL(k_depth_vis<false>, g, dim3(256), 0, st, depth, npx, F, range, lut, vis, range_out);
 }
 
 }  // namespace csg

@@ -9,12 +9,19 @@ frame a pure function of (seed, frame)), and host writer threads emit the
 same files:
 
   rgb/rgb_%06d.png                 (:1672-1673)
-  labels/label_%06d.json           (:2071-2072, schema :2056-2064 + keypoints_2d)
+  labels/label_%06d.json           (:2071-2072, schema :2056-2064 + keypoints_2d,
+                                    bbox_2d, pixel_count, occlusion_ratio)
   labels/instance_mask_%06d.npy    (:2066-2069; real ids here, -1 background)
-  depth/depth_%06d.npy|.csv        (:1687-1688, optional)
+  depth/depth_%06d.csv             (:1687-1688)
+  depth/depth_%06d.png             (:1690-1709, JET colour map made on the GPU)
+  depth/depth_%06d.npy             (optional)
   pointcloud/pointcloud_%06d.txt   (:1716-1724, optional; points from the GPU resolve)
   normals/normals_%06d.npy         (C5 normals, f16, optional)
-  logs/generation_summary.json     (:2090)
+  logs/generation_summary.json     (:2090; statistics, frame_logs, counters)
+  logs/generation_detail.log       (:254-263, per-frame entries + report)
+
+The default outputs are the reference's (RGB PNG, depth CSV + PNG, mask
+.npy, label JSON); ``--outputs`` picks others.
 
 Sharding: ``--rank/--world`` (or RANK/WORLD_SIZE) pick the epochs this
 process owns (shard.shard_of_range); no communication between shards.
@@ -28,6 +35,7 @@ import argparse
 import json
 import os
 import sys
+import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
@@ -78,25 +86,58 @@ def default_writers() -> int:
     return max(1, min(n, omp) if omp else n)
 
 
+OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png", "depth_npy", "pointcloud", "normals")
+# What the reference writes for every frame (GDP:1668-1711, 2055-2072): RGB PNG, depth CSV and
+# JET depth PNG, instance mask .npy; the label JSON is always written (it is the resume marker).
+REFERENCE_OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png")
+
+
+def parse_outputs(spec: str) -> tuple:
+    if spec in ("reference", ""):
+        return REFERENCE_OUTPUTS
+    if spec == "all":
+        return OUTPUTS
+    out = tuple(x.strip() for x in spec.split(",") if x.strip())
+    bad = [x for x in out if x not in OUTPUTS]
+    if bad:
+        raise ValueError(f"unknown outputs {bad}; choose from {OUTPUTS}")
+    return out
+
+
 def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 30,
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
-             resume: bool = True, normals: bool = False) -> dict:
+             resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None) -> dict:
+    """Render ``frames`` on one GPU and write them (``outputs``, default the
+    reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
+    add the depth .npy, the depth .npy + CSV, the point cloud, the normals)."""
+    outs = set(REFERENCE_OUTPUTS if outputs is None else outputs)
+    if depth or depth_csv:
+        outs.add("depth_npy")
+    if depth_csv:
+        outs.add("depth_csv")
+    if pointcloud:
+        outs.add("pointcloud")
+    if normals:
+        outs.add("normals")
     wl = Workload(workload, seed=seed, width=width, height=height)
     for d in ("rgb", "labels", "depth", "pointcloud", "normals", "logs"):
         os.makedirs(os.path.join(out_dir, d), exist_ok=True)
     if resume:
         frames = [f for f in frames if not os.path.exists(os.path.join(out_dir, "labels", f"label_{f:06d}.json"))]
-    depth = depth or depth_csv
+    host_depth = bool(outs & {"depth_csv", "depth_npy", "pointcloud"})
     log = QualityLog(os.path.join(out_dir, "logs"))
     r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
     intr = wl.intr
-    want = (["rgb", "instance", "keypoints", "stats"] + (["depth"] if depth else [])
-            + (["points"] if pointcloud else []) + (["normals"] if normals else []))
+    want = (["rgb", "instance", "keypoints", "stats", "covered"] + (["depth"] if host_depth else [])
+            + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
+            + (["normals"] if "normals" in outs else []))
     pose_cache = {}
     n_writers = writers or default_writers()
     pool = ThreadPoolExecutor(max_workers=n_writers)
     pending = []
+    t_render = 0.0
+    t0 = time.time()
     for s0 in range(0, len(frames), batch):
         fb = frames[s0:s0 + batch]
         epochs = sorted({f // 10 for f in fb})
@@ -112,26 +153,35 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             if e not in pose_cache:
                 pose_cache[e] = object_poses(wl.scene, st.object_frames)
         views, projs = wl.frame_params(fb)
+        tr = time.time()
         out = r.render(make_frames(views, projs, [set_of[f // 10] for f in fb], fb), want=want)
+        t_render += time.time() - tr
         for k, f in enumerate(fb):
             V, P, C, cam, aim, q = wl.camera(f)
             lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
                                out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
-                               wl.kp_table, wl.height, wl.width)
-            log.frame(lab["num_objects"], out["depth"][k] if "depth" in out else None, out["keypoints_vis"][k])
-            files = [(os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), _write_png, (out["rgb"][k],)),
-                     (os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"), fileio.write_npy,
-                      (out["instance"][k],))]
-            if depth:
-                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"), fileio.write_npy,
-                              (out["depth"][k],)))
-                if depth_csv:
-                    files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), fileio.write_depth_csv,
-                                  (out["depth"][k],)))
-            if pointcloud:
+                               wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k])
+            dk = out["depth"][k] if "depth" in out else None
+            log.frame(lab["num_objects"], dk, out["keypoints_vis"][k], frame_id=f, cam_pos=cam,
+                      depth_range=out["depth_range"][k] if "depth_range" in out else None,
+                      points=int(np.isfinite(dk).sum()) if "pointcloud" in outs else None)
+            files = []
+            if "rgb" in outs:
+                files.append((os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), _write_png, (out["rgb"][k],)))
+            if "mask" in outs:
+                files.append((os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"), fileio.write_npy,
+                              (out["instance"][k],)))
+            if "depth_npy" in outs:
+                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"), fileio.write_npy, (dk,)))
+            if "depth_csv" in outs:
+                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), fileio.write_depth_csv, (dk,)))
+            if "depth_png" in outs:
+                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.png"), _write_png,
+                              (out["depth_vis"][k],)))
+            if "pointcloud" in outs:
                 files.append((os.path.join(out_dir, "pointcloud", f"pointcloud_{f:06d}.txt"), _write_pointcloud,
                               (out["points"][k], out["rgb"][k])))
-            if normals:
+            if "normals" in outs:
                 files.append((os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), fileio.write_npy,
                               (out["normals"][k],)))
             pending.append(pool.submit(_write_frame, files, lab,
@@ -142,9 +192,14 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     for p in pending:
         p.result()
     pool.shutdown()
+    wall = time.time() - t0
     r.close()
     log.save()
-    return log.summary()
+    summary = log.summary()
+    summary["throughput"] = {"frames": len(frames), "wall_s": round(wall, 3), "render_s": round(t_render, 3),
+                             "frames_per_s": round(len(frames) / wall, 2) if wall > 0 else None,
+                             "writers": n_writers, "outputs": sorted(outs)}
+    return summary
 
 
 def main(argv=None):
@@ -159,16 +214,20 @@ def main(argv=None):
     ap.add_argument("--device", type=int, default=int(os.environ.get("LOCAL_RANK", "0")))
     ap.add_argument("--width", type=int)
     ap.add_argument("--height", type=int)
-    ap.add_argument("--depth", action="store_true")
-    ap.add_argument("--depth-csv", action="store_true")
+    ap.add_argument("--outputs", default="reference",
+                    help=f"'reference' ({','.join(REFERENCE_OUTPUTS)}), 'all', or a comma list of {OUTPUTS}")
+    ap.add_argument("--depth", action="store_true", help="add depth .npy")
+    ap.add_argument("--depth-csv", action="store_true", help="add depth .npy and CSV")
     ap.add_argument("--pointcloud", action="store_true")
     ap.add_argument("--normals", action="store_true")
+    ap.add_argument("--writers", type=int, default=0, help="writer threads (0: the CPUs this process may use)")
     ap.add_argument("--no-resume", action="store_true")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
-                       a.width, a.height, resume=not a.no_resume, normals=a.normals)
+                       a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
+                       outputs=parse_outputs(a.outputs))
     print(json.dumps(summary))
 
 

@@ -29,8 +29,33 @@ BBOX3D_DTYPE = np.dtype([("semanticId", "<u4"), ("x_min", "<f4"), ("y_min", "<f4
                          ("occlusionRatio", "<f4")])
 
 
-def bbox3d_records(scene, object_frames: Sequence[np.ndarray]) -> np.ndarray:
-    """Replicator-style bounding_box_3d data for every labelled object."""
+COVERED_UNKNOWN = 0x80000000   # csg_outputs.label_covered flag (a tile held more than 32 labels)
+
+
+def occlusion_ratios(pixels: np.ndarray, covered: np.ndarray) -> np.ndarray:
+    """Per label ``1 - visible / covered`` (Replicator's bounding_box_3d
+    ``occlusionRatio``, GDP:1780-1790: 0 fully visible, 1 fully occluded).
+    ``pixels`` = visible pixel count (inst_stats[:, 0]), ``covered`` = the
+    GPU's unoccluded coverage (label_covered); -1 where the coverage is
+    unknown or the label covers nothing in the frame."""
+    pixels = np.asarray(pixels, np.float64)
+    covered = np.asarray(covered, np.uint32)
+    known = (covered & COVERED_UNKNOWN) == 0
+    cnt = (covered & ~np.uint32(COVERED_UNKNOWN)).astype(np.float64)
+    ok = known & (cnt > 0)
+    out = np.full(covered.shape, -1.0, np.float32)
+    out[ok] = (1.0 - pixels[ok] / cnt[ok]).astype(np.float32)
+    return out
+
+
+def bbox3d_records(scene, object_frames: Sequence[np.ndarray], inst_stats: Optional[np.ndarray] = None,
+                   covered: Optional[np.ndarray] = None) -> np.ndarray:
+    """Replicator-style bounding_box_3d data for every labelled object;
+    ``occlusionRatio`` from the frame's label statistics and coverage when
+    given (else -1)."""
+    occ = None
+    if inst_stats is not None and covered is not None:
+        occ = occlusion_ratios(np.asarray(inst_stats)[:, 0], covered)
     rec = np.zeros(len(scene.objects), BBOX3D_DTYPE)
     for j, o in enumerate(scene.objects):
         lo, hi = o.local_bounds if o.local_bounds is not None else (np.zeros(3), np.zeros(3))
@@ -38,7 +63,7 @@ def bbox3d_records(scene, object_frames: Sequence[np.ndarray]) -> np.ndarray:
         rec[j]["x_min"], rec[j]["y_min"], rec[j]["z_min"] = lo
         rec[j]["x_max"], rec[j]["y_max"], rec[j]["z_max"] = hi
         rec[j]["transform"] = np.asarray(object_frames[j]).T       # USD row-vector convention
-        rec[j]["occlusionRatio"] = -1.0
+        rec[j]["occlusionRatio"] = occ[o.inst_idx] if occ is not None and o.inst_idx < occ.shape[0] else -1.0
     return rec
 
 
@@ -70,8 +95,11 @@ def object_poses(scene, object_frames) -> List[dict]:
 
 def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dict, poses: List[dict],
                  inst_stats: Optional[np.ndarray], kp_uv: Optional[np.ndarray], kp_vis: Optional[np.ndarray],
-                 kp_table: Optional[Sequence], height: int, width: int) -> dict:
-    """The label JSON of one frame (:2056-2064) for the objects visible in it."""
+                 kp_table: Optional[Sequence], height: int, width: int,
+                 covered: Optional[np.ndarray] = None) -> dict:
+    """The label JSON of one frame (:2056-2064) for the objects visible in it
+    (+ ``occlusion_ratio`` per object when the coverage is given)."""
+    occ = occlusion_ratios(inst_stats[:, 0], covered) if inst_stats is not None and covered is not None else None
     objs = []
     kp_by_obj: Dict[int, list] = {}
     if kp_uv is not None and kp_table is not None:
@@ -88,6 +116,8 @@ def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dic
             st = inst_stats[p["inst_idx"]]
             e["pixel_count"] = int(st[0])
             e["bbox_2d"] = [int(st[1]), int(st[2]), int(st[3]), int(st[4])]
+            if occ is not None:
+                e["occlusion_ratio"] = float(occ[p["inst_idx"]])
         if j in kp_by_obj:
             e["keypoints_2d"] = kp_by_obj[j]
         objs.append(e)

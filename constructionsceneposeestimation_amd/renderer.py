@@ -24,7 +24,7 @@ from .scene.model import Scene
 FRAME_DTYPE = np.dtype([("view", "<f4", 16), ("proj", "<f4", 16), ("xform_set", "<u4"), ("frame_id", "<u4")])
 assert FRAME_DTYPE.itemsize == C.sizeof(_lib.Frame)
 
-OUTPUT_KINDS = ("rgb", "instance", "depth", "keypoints", "stats")
+OUTPUT_KINDS = ("rgb", "instance", "depth", "keypoints", "stats", "normals", "points", "depth_vis", "covered")
 
 
 def make_frames(views: np.ndarray, projs: np.ndarray, sets: Sequence[int], frame_ids: Sequence[int]) -> np.ndarray:
@@ -174,12 +174,19 @@ class Renderer:
             out["normals"] = np.empty((n, H, W, 3), np.float16)
         if "points" in want:
             out["points"] = np.empty((n, H, W, 3), np.float32)
+        if "depth_vis" in want:   # the reference's JET depth PNG (GDP:1690-1709) and its min / max
+            out["depth_vis"] = np.empty((n, H, W, 3), np.uint8)
+            out["depth_range"] = np.empty((n, 2), np.float32)
+        if "covered" in want:     # unoccluded pixels per label (occlusionRatio)
+            out["label_covered"] = np.empty((n, self.n_labels), np.uint32)
         for s in range(0, n, self.max_frames):
             e = min(n, s + self.max_frames)
             oo = _lib.Outputs()
             for name, key in (("rgb", "rgb"), ("instance", "instance"), ("depth", "depth"),
                               ("keypoints_uv", "keypoints_uv"), ("keypoints_vis", "keypoints_vis"),
-                              ("inst_stats", "inst_stats"), ("normals", "normals"), ("points", "points")):
+                              ("inst_stats", "inst_stats"), ("normals", "normals"), ("points", "points"),
+                              ("depth_vis", "depth_vis"), ("depth_range", "depth_range"),
+                              ("label_covered", "label_covered")):
                 arr = out.get(key)
                 if arr is not None:
                     setattr(oo, name, arr[s:e].ctypes.data)
@@ -190,10 +197,12 @@ class Renderer:
 
     def render_into(self, frames_ptr: int, n: int, frames_on_device: bool, rgb: int = 0, instance: int = 0,
                     depth: int = 0, kp_uv: int = 0, kp_vis: int = 0, stats: int = 0, stream: int = 0,
-                    normals: int = 0, points: int = 0) -> None:
+                    normals: int = 0, points: int = 0, depth_vis: int = 0, depth_range: int = 0,
+                    covered: int = 0) -> None:
         """Enqueue a batch writing device buffers (raw pointers, e.g. torch ``data_ptr()``)."""
         o = _lib.Outputs(rgb or None, instance or None, depth or None, kp_uv or None, kp_vis or None,
-                         stats or None, self.n_labels, 1, normals or None, points or None)
+                         stats or None, self.n_labels, 1, normals or None, points or None, depth_vis or None,
+                         depth_range or None, covered or None)
         self._check(self.lib.csg_render_batch_async(self.ctx, frames_ptr, n, int(frames_on_device), C.byref(o),
                                                     stream or None), "render_batch_async")
 

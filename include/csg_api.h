@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 6
+#define CSG_ABI_VERSION 7
 
 typedef enum {
   CSG_OK = 0,
@@ -118,6 +118,15 @@ typedef struct {
                                 the camera; 0 where nothing is hit (C5 normals) */
   float* points;             /* [n][H][W][3] world-space point of each pixel from its depth
                                 (depth_to_pointcloud GDP:616-711, fused); NaN where no hit */
+  uint8_t* depth_vis;        /* [n][H][W][3] RGB: the reference's depth PNG (GDP:1690-1709):
+                                valid depth (finite, > 0) normalised by the frame's min / max,
+                                JET colour map (OpenCV COLORMAP_JET), black if nothing is hit */
+  float* depth_range;        /* [n][2] min, max of the valid depth (NaN, NaN: nothing hit) */
+  uint32_t* label_covered;   /* [n][n_labels] pixels each label would cover unoccluded: a
+                                fragment of it covers the centre, lies in the depth range and
+                                passes the alpha test (no depth test).  Bit 31 set = unknown
+                                (a 32x32 tile held more than 32 labels).  occlusionRatio =
+                                1 - pixels / covered (bounding_box_3d, GDP:1780-1790) */
 } csg_outputs;
 
 typedef struct {

@@ -141,10 +141,32 @@ static inline void interp_uv(const float e[3], float s, const float uv[3][2], fl
   *v = (l0 * uv[0][1] + l1 * uv[1][1]) + l2 * uv[2][1];
 }
 
+/* Label coverage for occlusion: per label, the pixels a
+ * fragment of it covers (centre covered, depth in range, alpha test passed;
+ * no depth test), and per 32x32 tile the labels that have such a fragment. */
+#define COV_TILE 32
+#define COV_SLOTS 32
+#define COV_UNKNOWN 0x80000000u
+typedef struct {
+  uint8_t* bits;        /* [n_labels][H*W] bit per pixel */
+  uint8_t* tile;        /* [n_tiles][n_labels] */
+  uint32_t n_labels, tiles_x, tiles_y;
+} cov_t;
+
+static int alpha_passes(const oracle_scene* s, const oracle_material* mat, const float e[3], float ssum,
+                        const float uv[3][2]) {
+  if (!(mat->alpha_test && mat->texture >= 0)) return 1;
+  float u, v;
+  int c[4];
+  interp_uv(e, ssum, uv, &u, &v);
+  tex_sample(s, mat->texture, u, v, c);
+  return c[3] > (int)mat->alpha_threshold;
+}
+
 /* Rasterise one screen triangle (fixed point) for the original triangle `uid`. */
 static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3], const float sv[3],
                        const hom_t* h, uint32_t uid, const oracle_material* mat,
-                       const float uv[3][2], oracle_stats* st) {
+                       const float uv[3][2], oracle_stats* st, cov_t* cv) {
   const int W = (int)s->width, H = (int)s->height;
   int32_t x[3], y[3];
   for (int k = 0; k < 3; ++k) {
@@ -198,6 +220,14 @@ static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3],
       hom_eval(h, px, py, e, &ssum, &invw);
       if (!(invw >= inv_far && invw <= inv_near)) continue;
       st->n_fragments++;
+      if (cv) {
+        const int32_t lab = s->inst_label[uid >> UID_SHIFT];
+        if (lab >= 0 && (uint32_t)lab < cv->n_labels && alpha_passes(s, mat, e, ssum, uv)) {
+          const size_t bit = (size_t)lab * W * H + (size_t)py * W + px;
+          cv->bits[bit >> 3] |= (uint8_t)(1u << (bit & 7));
+          cv->tile[((size_t)(py / COV_TILE) * cv->tiles_x + px / COV_TILE) * cv->n_labels + lab] = 1;
+        }
+      }
       const uint64_t key = ((uint64_t)(0xFFFFFFFFu - fbits(invw)) << 32) | uid;
       uint64_t* z = &zbuf[(size_t)py * W + px];
       if (key >= *z) { st->n_early_z_killed++; continue; }
@@ -280,15 +310,64 @@ int oracle_render_frame(const oracle_scene* s, const float* view, const float* p
 int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float* proj,
                            uint8_t* rgb, int32_t* inst, float* depth, uint16_t* normals, float* points,
                            uint32_t* inst_stats, uint32_t n_labels, oracle_stats* st_out) {
+  return oracle_render_frame_cov(s, view, proj, rgb, inst, depth, normals, points, inst_stats, NULL, n_labels,
+                                 st_out);
+}
+
+/* covered[l] from the coverage bits: tiles holding more than COV_SLOTS labels
+ * flag their labels unknown and add no counts (the GPU's tile table). */
+static void cov_finish(const cov_t* cv, int W, int H, uint32_t* covered) {
+  for (uint32_t l = 0; l < cv->n_labels; ++l) covered[l] = 0;
+  for (uint32_t ty = 0; ty < cv->tiles_y; ++ty) {
+    for (uint32_t tx = 0; tx < cv->tiles_x; ++tx) {
+      const uint8_t* tl = cv->tile + ((size_t)ty * cv->tiles_x + tx) * cv->n_labels;
+      uint32_t n = 0;
+      for (uint32_t l = 0; l < cv->n_labels; ++l) n += tl[l];
+      for (uint32_t l = 0; l < cv->n_labels; ++l) {
+        if (!tl[l]) continue;
+        if (n > COV_SLOTS) { covered[l] |= COV_UNKNOWN; continue; }
+        uint32_t cnt = 0;
+        for (int py = (int)ty * COV_TILE; py < (int)(ty + 1) * COV_TILE && py < H; ++py)
+          for (int px = (int)tx * COV_TILE; px < (int)(tx + 1) * COV_TILE && px < W; ++px) {
+            const size_t bit = (size_t)l * W * H + (size_t)py * W + px;
+            cnt += (cv->bits[bit >> 3] >> (bit & 7)) & 1u;
+          }
+        covered[l] += cnt;
+      }
+    }
+  }
+}
+
+int oracle_render_frame_cov(const oracle_scene* s, const float* view, const float* proj,
+                            uint8_t* rgb, int32_t* inst, float* depth, uint16_t* normals, float* points,
+                            uint32_t* inst_stats, uint32_t* label_covered, uint32_t n_labels,
+                            oracle_stats* st_out) {
   const int W = (int)s->width, H = (int)s->height;
   uint64_t* zbuf = (uint64_t*)malloc((size_t)W * H * sizeof(uint64_t));
   if (!zbuf) return -1;
+  cov_t cov_store, *cv = NULL;
+  if (label_covered && n_labels) {
+    cov_store.n_labels = n_labels;
+    cov_store.tiles_x = (uint32_t)(W + COV_TILE - 1) / COV_TILE;
+    cov_store.tiles_y = (uint32_t)(H + COV_TILE - 1) / COV_TILE;
+    cov_store.bits = (uint8_t*)calloc(((size_t)n_labels * W * H + 7) / 8, 1);
+    cov_store.tile = (uint8_t*)calloc((size_t)cov_store.tiles_x * cov_store.tiles_y * n_labels, 1);
+    if (!cov_store.bits || !cov_store.tile) {
+      free(cov_store.bits); free(cov_store.tile); free(zbuf);
+      return -1;
+    }
+    cv = &cov_store;
+  }
   for (size_t i = 0; i < (size_t)W * H; ++i) zbuf[i] = EMPTY_KEY;
   oracle_stats st;
   memset(&st, 0, sizeof(st));
-  if (s->n_inst >= (1u << (32 - UID_SHIFT))) { free(zbuf); return -2; }
-  for (uint32_t i = 0; i < s->n_inst; ++i)
-    if (s->meshes[s->inst_mesh[i]].ntris >= (1u << UID_SHIFT)) { free(zbuf); return -2; }
+  int limit = s->n_inst >= (1u << (32 - UID_SHIFT));
+  for (uint32_t i = 0; i < s->n_inst; ++i) limit |= s->meshes[s->inst_mesh[i]].ntris >= (1u << UID_SHIFT);
+  if (limit) {
+    if (cv) { free(cv->bits); free(cv->tile); }
+    free(zbuf);
+    return -2;
+  }
   const float near = s->near_clip, far = s->far_clip;
   const float Wf = (float)W, Hf = (float)H;
 
@@ -323,7 +402,7 @@ int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float
           su[k] = v[k].x * rw;
           sv[k] = v[k].y * rw;
         }
-        raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st);
+        raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st, cv);
       } else {
         /* Sutherland-Hodgman against W >= near, edges v0->v1, v1->v2, v2->v0 */
         st.n_clipped++;
@@ -350,12 +429,17 @@ int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float
             su[k] = tri3[k].x * rw;
             sv[k] = tri3[k].y * rw;
           }
-          raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st);
+          raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st, cv);
         }
       }
     }
   }
 
+  if (cv) {
+    cov_finish(cv, W, H, label_covered);
+    free(cv->bits);
+    free(cv->tile);
+  }
   /* resolve */
   float cam[16];
   frame_camera(view, proj, cam);

@@ -81,6 +81,15 @@ int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float
                            uint8_t* rgb, int32_t* inst, float* depth, uint16_t* normals, float* points,
                            uint32_t* inst_stats, uint32_t n_labels, oracle_stats* st);
 
+/* Same plus the label coverage of the occlusion ratio: label_covered
+ * [n_labels] = pixels each label covers with a fragment in the depth range
+ * that passes its alpha test (no depth test); a 32x32 tile with more than 32
+ * such labels flags them with bit 31 and adds no counts. */
+int oracle_render_frame_cov(const oracle_scene* s, const float* view, const float* proj,
+                            uint8_t* rgb, int32_t* inst, float* depth, uint16_t* normals, float* points,
+                            uint32_t* inst_stats, uint32_t* label_covered, uint32_t n_labels,
+                            oracle_stats* st);
+
 /* Project world keypoints; visibility against a rendered depth buffer.
  * uv: [n][2], vis: [n] (0 out/behind, 1 occluded, 2 visible). */
 int oracle_keypoints(const oracle_scene* s, const float* view, const float* proj,

@@ -57,6 +57,8 @@ def lib():
         _lib.oracle_render_frame.argtypes = [C.POINTER(_Scene), vp, vp, vp, vp, vp, vp, u32, C.POINTER(_Stats)]
         _lib.oracle_render_frame_ex.argtypes = [C.POINTER(_Scene), vp, vp, vp, vp, vp, vp, vp, vp, u32,
                                                 C.POINTER(_Stats)]
+        _lib.oracle_render_frame_cov.argtypes = [C.POINTER(_Scene), vp, vp, vp, vp, vp, vp, vp, vp, vp, u32,
+                                                 C.POINTER(_Stats)]
         _lib.oracle_keypoints.argtypes = [C.POINTER(_Scene), vp, vp, vp, u32, vp, vp, vp]
         _lib.oracle_render_frames.argtypes = [C.POINTER(_Scene), vp, vp, u32, vp, vp, vp, vp, C.c_int]
         _lib.oracle_mat4_mul.argtypes = [vp, vp, vp]
@@ -133,9 +135,12 @@ class Oracle:
         self._keep.append(a)
         self.s.inst_model = a.ctypes.data
 
-    def render(self, view: np.ndarray, proj: np.ndarray, want_stats: bool = False, extra: bool = False):
+    def render(self, view: np.ndarray, proj: np.ndarray, want_stats: bool = False, extra: bool = False,
+               covered: bool = False):
         """One frame; ``extra`` adds the C5 outputs ``normals`` (H,W,3 float16)
-        and ``points`` (H,W,3 float32 world xyz, NaN where nothing is hit)."""
+        and ``points`` (H,W,3 float32 world xyz, NaN where nothing is hit);
+        ``covered`` adds ``label_covered`` (n_labels,) uint32, the occlusion
+        coverage (csg_outputs.label_covered)."""
         H, W = self.height, self.width
         rgb = np.empty((H, W, 3), np.uint8)
         inst = np.empty((H, W), np.int32)
@@ -147,11 +152,14 @@ class Oracle:
         st = _Stats()
         v = np.ascontiguousarray(view, np.float32).reshape(16)
         pr = np.ascontiguousarray(proj, np.float32).reshape(16)
-        rc = lib().oracle_render_frame_ex(C.byref(self.s), _ptr(v), _ptr(pr), _ptr(rgb), _ptr(inst), _ptr(depth),
-                                          _ptr(normals), _ptr(points), _ptr(stats), nl, C.byref(st))
+        cov = np.empty(nl, np.uint32) if covered else None
+        rc = lib().oracle_render_frame_cov(C.byref(self.s), _ptr(v), _ptr(pr), _ptr(rgb), _ptr(inst), _ptr(depth),
+                                           _ptr(normals), _ptr(points), _ptr(stats), _ptr(cov), nl, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_render_frame failed: {rc}")
         out = {"rgb": rgb, "instance": inst, "depth": depth, "inst_stats": stats}
+        if covered:
+            out["label_covered"] = cov
         if extra:
             out["normals"], out["points"] = normals, points
         if want_stats:
@@ -193,3 +201,42 @@ def mat4_mul_f32(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     c = np.empty(16, np.float32)
     lib().oracle_mat4_mul(_ptr(a), _ptr(b), _ptr(c))
     return c.reshape(4, 4)
+
+
+# ---------------------------------------------------------------------------
+# Depth visualisation (generate_construction_data.py:1690-1709), restated in
+# NumPy with the promotion rules of NumPy 1.x, the version Isaac Sim ships:
+# ``depth_max - depth_min + 1e-6`` is a float64 scalar there (a float32 scalar
+# plus a Python float), and dividing the float32 array by it casts it back to
+# float32.  ``cv2.applyColorMap(..., COLORMAP_JET)`` is restated as the GNU
+# Octave jet map OpenCV documents, sampled at k/255, stored as float32, scaled
+# by 255 in float32 and rounded half to even (OpenCV is absent here: the table
+# is unpinned against cv2).
+# ---------------------------------------------------------------------------
+def jet_lut() -> np.ndarray:
+    """(256, 3) uint8 RGB."""
+    x = np.arange(256, dtype=np.float64) / 255.0
+    r = np.where((x >= 3 / 8) & (x < 5 / 8), 4 * x - 1.5,
+                 np.where((x >= 5 / 8) & (x < 7 / 8), 1.0, np.where(x >= 7 / 8, -4 * x + 4.5, 0.0)))
+    g = np.where((x >= 1 / 8) & (x < 3 / 8), 4 * x - 0.5,
+                 np.where((x >= 3 / 8) & (x < 5 / 8), 1.0, np.where((x >= 5 / 8) & (x < 7 / 8), -4 * x + 3.5, 0.0)))
+    b = np.where(x < 1 / 8, 4 * x + 0.5,
+                 np.where((x >= 1 / 8) & (x < 3 / 8), 1.0, np.where((x >= 3 / 8) & (x < 5 / 8), -4 * x + 2.5, 0.0)))
+    lut = np.stack([r, g, b], 1).astype(np.float32) * np.float32(255.0)
+    return np.clip(np.rint(lut), 0, 255).astype(np.uint8)
+
+
+def depth_vis(depth: np.ndarray):
+    """(H, W, 3) uint8 RGB JET image and (min, max) of one depth map."""
+    depth = np.asarray(depth, np.float32)
+    mask = np.isfinite(depth) & (depth > 0)
+    if not mask.any():
+        return np.zeros(depth.shape + (3,), np.uint8), (float("nan"), float("nan"))
+    dmin = np.float32(depth[mask].min())
+    dmax = np.float32(depth[mask].max())
+    den = np.float32(np.float64(np.float32(dmax - dmin)) + 1e-6)
+    idx = np.zeros(depth.shape, np.uint8)
+    q = (depth[mask] - dmin) / den
+    idx[mask] = (q * np.float32(255)).astype(np.uint8)
+    return jet_lut()[idx], (float(dmin), float(dmax))
+

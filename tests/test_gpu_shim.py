@@ -100,6 +100,21 @@ def test_generate_writes_reference_layout(tmp_path):
     nrm = np.load(tmp_path / "normals" / "normals_000003.npy")
     assert nrm.dtype == np.float16 and nrm.shape == (96, 160, 3)
     assert os.path.exists(tmp_path / "logs" / "generation_summary.json")
+    # the reference's default set: depth CSV + JET depth PNG (GDP:1687-1709), decoded == the oracle's map
+    from PIL import Image
+    from oracle.oracle import depth_vis
+    import io
+    buf = io.StringIO()
+    np.savetxt(buf, d3, delimiter=" ", fmt="%.6f")
+    assert (tmp_path / "depth" / "depth_000003.csv").read_text() == buf.getvalue()
+    png = np.asarray(Image.open(tmp_path / "depth" / "depth_000003.png").convert("RGB"))
+    assert np.array_equal(png, depth_vis(d3)[0])
+    for o in lab["objects"]:
+        assert 0.0 <= o["occlusion_ratio"] <= 1.0
+    summ = json.load(open(tmp_path / "logs" / "generation_summary.json"))
+    assert len(summ["frame_logs"]) == 12 and summ["statistics"]["successful_frames"] == 12
+    assert summ["frame_logs"][3]["depth"]["valid_pixels"] == int(np.isfinite(d3).sum())
+    assert "frame 11 done" in open(tmp_path / "logs" / "generation_detail.log").read()
     # resume: nothing left to do
     again = generate(str(tmp_path), list(range(12)), "C3", seed=1, batch=5, width=160, height=96)
     assert again["counters"]["total_attempts"] == 0
