@@ -46,14 +46,81 @@ void png_chunk(std::vector<uint8_t>& out, const char* type, const uint8_t* data,
   put_be32(out, crc);
 }
 
-// "%.6f" of a double, as printf in the C locale (std::to_chars is specified so).
+// "%.6f" of a double, as Python's % operator formats it for np.savetxt
+// (std::to_chars is correctly rounded, ties to even, like Python's dtoa;
+// NaN prints as "nan" whatever its sign bit, as Python does).
 inline char* fmt6(char* p, char* end, double x) {
   if (std::isnan(x)) {
-    if (std::signbit(x)) *p++ = '-';
     std::memcpy(p, "nan", 3);
     return p + 3;
   }
   return std::to_chars(p, end, x, std::chars_format::fixed, 6).ptr;
+}
+
+// "00" "01" ... "99"
+constexpr char kDigits2[201] =
+    "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+    "8081828384858687888990919293949596979899";
+
+// Decimal digits of v (v < 10^20), most significant first.
+inline char* put_u64(char* p, uint64_t v) {
+  char tmp[20];
+  int n = 0;
+  do {
+    tmp[n++] = (char)('0' + v % 10u);
+    v /= 10u;
+  } while (v);
+  while (n) *p++ = tmp[--n];
+  return p;
+}
+
+// "%.6f" of a float32 value, exactly as fmt6 of its double: the value is
+// m * 2^e with a 24-bit m, so x * 10^6 = m * 10^6 * 2^e is an integer (m *
+// 10^6 < 2^44) shifted right by -e, rounded half to even from the exact
+// remainder -- no floating point, about 4x faster than to_chars.  Values of
+// 2^40 and above take fmt6.
+inline char* fmt6f(char* p, char* end, float x) {
+  uint32_t u;
+  std::memcpy(&u, &x, 4);
+  const uint32_t ex = (u >> 23) & 255u, mant = u & 0x7FFFFFu;
+  if (ex == 255u || ex >= 127u + 40u) return fmt6(p, end, (double)x);   // inf, nan, huge
+  const uint64_t m = ex ? (mant | 0x800000u) : mant;
+  const int e = ex ? (int)ex - 150 : -149;
+  if (u >> 31) *p++ = '-';
+  uint64_t q;
+  if (e >= 0) {
+    q = (m << e) * 1000000u;   // an integer: < 2^64 / 10^6 here
+  } else {
+    const uint64_t n = m * 1000000u;
+    const int sh = -e;
+    if (sh >= 64) {
+      q = 0;                   // n < 2^44 <= half
+    } else {
+      q = n >> sh;
+      const uint64_t r = n & ((1ull << sh) - 1u), half = 1ull << (sh - 1);
+      if (r > half || (r == half && (q & 1u))) ++q;
+    }
+  }
+  const uint64_t ip = q / 1000000u;
+  const uint32_t f = (uint32_t)(q - ip * 1000000u);
+  if (ip < 10u) {
+    *p++ = (char)('0' + ip);
+  } else if (ip < 100u) {
+    std::memcpy(p, kDigits2 + 2 * ip, 2);
+    p += 2;
+  } else if (ip < 1000u) {
+    *p++ = (char)('0' + ip / 100u);
+    std::memcpy(p, kDigits2 + 2 * (ip % 100u), 2);
+    p += 2;
+  } else {
+    p = put_u64(p, ip);
+  }
+  *p++ = '.';
+  std::memcpy(p, kDigits2 + 2 * (f / 10000u), 2);
+  std::memcpy(p + 2, kDigits2 + 2 * ((f / 100u) % 100u), 2);
+  std::memcpy(p + 4, kDigits2 + 2 * (f % 100u), 2);
+  return p + 6;
 }
 
 }  // namespace
@@ -133,7 +200,7 @@ int csgio_write_depth_csv(const char* path, const float* d, uint32_t w, uint32_t
     char* end = line.data() + line.size();
     for (uint32_t x = 0; x < w; ++x) {
       if (x) *p++ = ' ';
-      p = fmt6(p, end, (double)d[(size_t)y * w + x]);
+      p = fmt6f(p, end, d[(size_t)y * w + x]);
     }
     *p++ = '\n';
     if (!f.write(line.data(), (size_t)(p - line.data()))) return -EIO;
@@ -159,11 +226,13 @@ int csgio_write_pointcloud_txt(const char* path, const float* xyz, const uint8_t
     char* p = buf.data() + used;
     char* end = buf.data() + buf.size();
     for (int c = 0; c < 3; ++c) {
-      p = fmt6(p, end, (double)p3[c]);
+      p = fmt6f(p, end, p3[c]);
       *p++ = ' ';
     }
     for (int c = 0; c < 3; ++c) {
-      p = fmt6(p, end, (double)rgb[3 * k + c]);
+      p = put_u64(p, rgb[3 * k + c]);   // "%.6f" of an integer
+      std::memcpy(p, ".000000", 7);
+      p += 7;
       *p++ = c < 2 ? ' ' : '\n';
     }
     used = (size_t)(p - buf.data());

@@ -74,3 +74,22 @@ def test_pointcloud_txt_identical_to_savetxt(tmp_path):
 def test_errors_are_raised(tmp_path):
     with pytest.raises(OSError):
         writers.write_png(str(tmp_path / "missing_dir" / "x.png"), np.zeros((2, 2, 3), np.uint8))
+
+
+def test_depth_csv_float32_fast_path_identical_to_savetxt(tmp_path):
+    """The integer %.6f formatter (exact m * 10^6 * 2^e, ties to even) on
+    random bit patterns, ties, subnormals, values near 2^40, +-0, inf, nan."""
+    import io
+    rng = np.random.default_rng(7)
+    bits = rng.integers(0, 2 ** 32, 200000, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    edge = np.array([0.0, -0.0, 1e-7, 5e-7, -5e-7, 0.0000015, 0.0000025, 122.0703125, 2 ** 40, 2 ** 40 - 2 ** 16,
+                     2 ** 39 + 0.5, 1.5e-45, -1.5e-45, np.inf, -np.inf, np.nan, -np.nan, 0.5, 999999.5, 9.9999995,
+                     99.99999, 999.99994, 1000.0, 16777215.0, 3.4e38, -3.4e38], np.float32)
+    vals = np.concatenate([bits, edge, (np.arange(50000) / 2 ** 20).astype(np.float32),
+                           rng.uniform(0.5, 250.0, 50000).astype(np.float32)])
+    vals = vals[: len(vals) // 6 * 6].reshape(-1, 6)
+    a = str(tmp_path / "a.csv")
+    writers.write_depth_csv(a, vals)
+    b = io.StringIO()
+    np.savetxt(b, vals, delimiter=" ", fmt="%.6f")
+    assert open(a).read() == b.getvalue()
