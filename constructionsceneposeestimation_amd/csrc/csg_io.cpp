@@ -129,8 +129,8 @@ extern "C" {
 
 int csgio_abi_version(void) { return CSGIO_ABI_VERSION; }
 
-int csgio_write_png_rgb(const char* path, const uint8_t* rgb, uint32_t w, uint32_t h, int level) {
-  if (!path || !rgb || !w || !h || level < 0 || level > 9) return -EINVAL;
+int csgio_write_png_rgb(const char* path, const uint8_t* rgb, uint32_t w, uint32_t h, int level, int strategy) {
+  if (!path || !rgb || !w || !h || level < 0 || level > 9 || strategy < 0 || strategy > 2) return -EINVAL;
   // filter type 1 (Sub) on every row: byte minus the byte one pixel to the left
   const size_t stride = (size_t)w * 3;
   std::vector<uint8_t> raw((stride + 1) * h);
@@ -143,7 +143,19 @@ int csgio_write_png_rgb(const char* path, const uint8_t* rgb, uint32_t w, uint32
   }
   uLongf zn = compressBound((uLong)raw.size());
   std::vector<uint8_t> z(zn);
-  if (compress2(z.data(), &zn, raw.data(), (uLong)raw.size(), level) != Z_OK) return -EIO;
+  {
+    z_stream zs{};
+    static const int kStrategy[3] = {Z_DEFAULT_STRATEGY, Z_RLE, Z_HUFFMAN_ONLY};
+    if (deflateInit2(&zs, level, Z_DEFLATED, 15, 9, kStrategy[strategy]) != Z_OK) return -EIO;
+    zs.next_in = raw.data();
+    zs.avail_in = (uInt)raw.size();
+    zs.next_out = z.data();
+    zs.avail_out = (uInt)zn;
+    const int rc = deflate(&zs, Z_FINISH);
+    zn = zs.total_out;
+    deflateEnd(&zs);
+    if (rc != Z_STREAM_END) return -EIO;
+  }
   std::vector<uint8_t> out;
   out.reserve(zn + 64);
   static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
@@ -206,6 +218,33 @@ int csgio_write_depth_csv(const char* path, const float* d, uint32_t w, uint32_t
     if (!f.write(line.data(), (size_t)(p - line.data()))) return -EIO;
   }
   return f.close();
+}
+
+int csgio_depth_stats(const float* d, uint64_t n, double* out) {
+  if ((!d && n) || !out) return -EINVAL;
+  uint64_t valid = 0, zero = 0, inf = 0;
+  double sum = 0.0;
+  float lo = INFINITY, hi = -INFINITY;
+  for (uint64_t k = 0; k < n; ++k) {
+    const float v = d[k];
+    if (v > 0.0f && v < INFINITY) {
+      ++valid;
+      sum += (double)v;
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    } else if (v == 0.0f) {
+      ++zero;
+    } else if (std::isinf(v)) {
+      ++inf;
+    }
+  }
+  out[0] = (double)valid;
+  out[1] = (double)zero;
+  out[2] = (double)inf;
+  out[3] = sum;
+  out[4] = valid ? (double)lo : 0.0;
+  out[5] = valid ? (double)hi : 0.0;
+  return 0;
 }
 
 int csgio_write_pointcloud_txt(const char* path, const float* xyz, const uint8_t* rgb, uint64_t n) {

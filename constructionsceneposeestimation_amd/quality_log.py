@@ -11,8 +11,9 @@ generate_construction_data.py:237-470).
   by summation (shard.merge_counters).
 
 The depth statistics take the GPU's per-frame min / max (``depth_range`` of
-the depth-visualisation kernels) when given; the counts and the mean are
-taken from the host depth array when the frame has one.
+the depth-visualisation kernels) when given; the counts and the mean come
+from one native pass over the host depth (writers.depth_stats), which the
+generator runs in its writer threads.
 """
 from __future__ import annotations
 
@@ -56,9 +57,12 @@ class QualityLog:
     # -- per frame -------------------------------------------------------------
     def frame(self, n_objects: int, depth: Optional[np.ndarray] = None, kp_vis: Optional[np.ndarray] = None,
               frame_id: Optional[int] = None, cam_pos: Optional[Sequence[float]] = None,
-              depth_range: Optional[Sequence[float]] = None, points: Optional[int] = None) -> dict:
+              depth_range: Optional[Sequence[float]] = None, points: Optional[int] = None,
+              depth_stats: Optional[dict] = None) -> dict:
         """Record one rendered frame (the reference's log_frame_start ...
-        log_frame_end sequence for a frame that succeeded)."""
+        log_frame_end sequence for a frame that succeeded).  The depth entry
+        comes from ``depth_stats`` (writers.depth_stats, computed by a writer
+        thread) or from the ``depth`` array."""
         rec = {"frame_id": int(frame_id) if frame_id is not None else self.c["total_attempts"],
                "camera_position": [float(x) for x in cam_pos] if cam_pos is not None else None,
                "retry_count": 0, "status": "processing", "issues": []}
@@ -69,8 +73,11 @@ class QualityLog:
         self.stats["rgb_stats"]["valid"] += 1
         rec["rgb"] = {"status": "valid"}
         msg.append("  + RGB ok\n")
-        if depth is not None:
-            self._depth(rec, msg, depth, depth_range)
+        if depth_stats is None and depth is not None:
+            from .writers import depth_stats as _stats
+            depth_stats = _stats(depth)
+        if depth_stats is not None:
+            self._depth(rec, msg, depth_stats, depth_range)
         if points is not None:
             if points > 0:
                 self.stats["pointcloud_stats"]["valid"] += 1
@@ -105,20 +112,17 @@ class QualityLog:
             self.flush()
         return rec
 
-    def _depth(self, rec: dict, msg: List[str], depth: np.ndarray, depth_range) -> None:
+    def _depth(self, rec: dict, msg: List[str], ds: dict, depth_range) -> None:
         self.c["depth_success"] += 1
-        fin = np.isfinite(depth)
-        valid = fin & (depth > 0)
-        n_valid, total = int(valid.sum()), int(depth.size)
-        zero, inf = int((depth == 0).sum()), int(np.isinf(depth).sum())
-        self.c["depth_valid_pixels"] += int(fin.sum())
+        n_valid, total, zero, inf = ds["valid"], ds["total"], ds["zero"], ds["inf"]
+        self.c["depth_valid_pixels"] += n_valid
         self.c["depth_total_pixels"] += total
         if n_valid:
             if depth_range is not None and np.isfinite(depth_range).all():
-                lo, hi = float(depth_range[0]), float(depth_range[1])
+                lo, hi = float(depth_range[0]), float(depth_range[1])   # the GPU's min / max (depth PNG)
             else:
-                lo, hi = float(depth[valid].min()), float(depth[valid].max())
-            mean = float(np.mean(depth[valid]))
+                lo, hi = ds["min"], ds["max"]
+            mean = ds["sum"] / n_valid                                  # float64 sum (the reference: np.mean)
         else:
             lo = hi = mean = 0.0
         rec["depth"] = {"status": "valid", "valid_pixels": n_valid, "total_pixels": total,

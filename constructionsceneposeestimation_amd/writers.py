@@ -16,9 +16,10 @@ import numpy as np
 
 from .build import IO_LIB, build_io, needs_build, IO_DEPS
 
-ABI_VERSION = 1  # CSGIO_ABI_VERSION in include/csg_io.h
+ABI_VERSION = 2  # CSGIO_ABI_VERSION in include/csg_io.h
 EXPORTED = ("csgio_abi_version", "csgio_write_png_rgb", "csgio_write_npy", "csgio_write_depth_csv",
-            "csgio_write_pointcloud_txt")
+            "csgio_write_pointcloud_txt", "csgio_depth_stats")
+PNG_STRATEGY = {"default": 0, "rle": 1, "huffman": 2}
 _lib: Optional[C.CDLL] = None
 
 
@@ -39,7 +40,8 @@ def load() -> C.CDLL:
     lib = C.CDLL(IO_LIB)
     vp, u32, u64, cp = C.c_void_p, C.c_uint32, C.c_uint64, C.c_char_p
     lib.csgio_abi_version.argtypes = []
-    lib.csgio_write_png_rgb.argtypes = [cp, vp, u32, u32, C.c_int]
+    lib.csgio_write_png_rgb.argtypes = [cp, vp, u32, u32, C.c_int, C.c_int]
+    lib.csgio_depth_stats.argtypes = [vp, u64, vp]
     lib.csgio_write_npy.argtypes = [cp, vp, u64, cp, vp, u32]
     lib.csgio_write_depth_csv.argtypes = [cp, vp, u32, u32]
     lib.csgio_write_pointcloud_txt.argtypes = [cp, vp, vp, u64]
@@ -54,10 +56,21 @@ def _check(rc: int, what: str, path: str) -> None:
         raise CsgIoError(-rc, f"{what} failed: {os.strerror(-rc)}", path)
 
 
-def write_png(path: str, rgb: np.ndarray, level: int = 1) -> None:
+def write_png(path: str, rgb: np.ndarray, level: int = 1, strategy: str = "default") -> None:
     a = np.ascontiguousarray(rgb, np.uint8)
     assert a.ndim == 3 and a.shape[2] == 3, a.shape
-    _check(load().csgio_write_png_rgb(path.encode(), a.ctypes.data, a.shape[1], a.shape[0], level), "write_png", path)
+    _check(load().csgio_write_png_rgb(path.encode(), a.ctypes.data, a.shape[1], a.shape[0], level,
+                                      PNG_STRATEGY[strategy]), "write_png", path)
+
+
+def depth_stats(depth: np.ndarray) -> dict:
+    """Counts of one depth image in one native pass (GIL released):
+    valid (finite, > 0), zero and infinite pixels, sum / min / max of the valid."""
+    a = np.ascontiguousarray(depth, np.float32)
+    out = np.zeros(6, np.float64)
+    _check(load().csgio_depth_stats(a.ctypes.data, a.size, out.ctypes.data), "depth_stats", "")
+    return {"valid": int(out[0]), "zero": int(out[1]), "inf": int(out[2]), "total": int(a.size),
+            "sum": float(out[3]), "min": float(out[4]), "max": float(out[5])}
 
 
 def write_npy(path: str, arr: np.ndarray) -> None:

@@ -22,14 +22,15 @@ def test_library_loads_and_exports():
     assert lib.csgio_abi_version() == writers.ABI_VERSION
 
 
+@pytest.mark.parametrize("strategy", ["default", "rle", "huffman"])
 @pytest.mark.parametrize("shape", [(1, 1), (17, 33), (96, 160)])
-def test_png_roundtrip(tmp_path, shape):
+def test_png_roundtrip(tmp_path, shape, strategy):
     from PIL import Image
     rng = np.random.default_rng(0)
     rgb = rng.integers(0, 256, shape + (3,), dtype=np.uint8)
     rgb[: shape[0] // 2] = [191, 217, 255]          # flat sky band
     p = str(tmp_path / "a.png")
-    writers.write_png(p, rgb, level=1)
+    writers.write_png(p, rgb, level=1, strategy=strategy)
     back = np.asarray(Image.open(p).convert("RGB"))
     assert np.array_equal(back, rgb)
 
@@ -93,3 +94,10 @@ def test_depth_csv_float32_fast_path_identical_to_savetxt(tmp_path):
     b = io.StringIO()
     np.savetxt(b, vals, delimiter=" ", fmt="%.6f")
     assert open(a).read() == b.getvalue()
+
+
+def test_depth_stats_one_pass():
+    d = np.array([[np.inf, 0.0, 2.5, -1.0], [np.nan, 4.0, 0.5, -np.inf]], np.float32)
+    st = writers.depth_stats(d)
+    assert st == {"valid": 3, "zero": 1, "inf": 2, "total": 8, "sum": 7.0, "min": 0.5, "max": 4.0}
+    assert writers.depth_stats(np.full((2, 2), np.inf, np.float32))["valid"] == 0
