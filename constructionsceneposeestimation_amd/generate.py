@@ -99,12 +99,7 @@ def _log_done(log: QualityLog, fut, log_args: dict, points: bool) -> None:
 OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png", "depth_npy", "pointcloud", "normals")
 # What the reference writes for every frame (GDP:1668-1711, 2055-2072): RGB PNG, depth CSV and
 # JET depth PNG, instance mask .npy; the label JSON is always written (it is the resume marker).
-REFERENCE_def _log_done(log: QualityLog, fut, log_args: dict, points: bool) -> None:
-    ds = fut.result()
-    log.frame(depth_stats=ds, points=ds["valid"] if points and ds else None, **log_args)
-
-
-OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png")
+REFERENCE_OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png")
 
 
 def parse_outputs(spec: str) -> tuple:

@@ -151,3 +151,12 @@ def test_domain_randomization_is_keyed_and_bounded(world2):
     assert len(seen) > 1
     c = schedule.domain_randomization(sc, 8, 5, var)
     assert not np.array_equal(c.light.sun_dir, schedule.domain_randomization(sc, 7, 5, var).light.sun_dir)
+
+
+def test_generate_cli_outputs_parse():
+    from constructionsceneposeestimation_amd.generate import OUTPUTS, REFERENCE_OUTPUTS, parse_outputs
+    assert parse_outputs("reference") == REFERENCE_OUTPUTS == ("rgb", "mask", "depth_csv", "depth_png")
+    assert parse_outputs("all") == OUTPUTS
+    assert parse_outputs("rgb, depth_npy") == ("rgb", "depth_npy")
+    with pytest.raises(ValueError):
+        parse_outputs("rgb,jpeg")
