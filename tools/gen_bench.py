@@ -39,10 +39,11 @@ def encode_costs(wl_name, out_dir, outputs):
     with Renderer(wl.scene, wl.width, wl.height, max_frames=1) as r:
         r.set_instance_transforms(0, wl.epoch(f // 10).models)
         o = r.render(make_frames(V, P, [0], [f]), want=("rgb", "instance", "depth", "depth_vis", "points"))
-    jobs = {"rgb": lambda p: fileio.write_png(p + ".png", o["rgb"][0], level=1),
+    from constructionsceneposeestimation_amd.generate import _write_png   # the generator's PNG settings
+    jobs = {"rgb": lambda p: _write_png(p + ".png", o["rgb"][0]),
             "mask": lambda p: fileio.write_npy(p + ".npy", o["instance"][0]),
             "depth_csv": lambda p: fileio.write_depth_csv(p + ".csv", o["depth"][0]),
-            "depth_png": lambda p: fileio.write_png(p + ".png", o["depth_vis"][0], level=1),
+            "depth_png": lambda p: _write_png(p + ".png", o["depth_vis"][0]),
             "depth_npy": lambda p: fileio.write_npy(p + ".npy", o["depth"][0]),
             "pointcloud": lambda p: fileio.write_pointcloud_txt(p + ".txt", o["points"][0], o["rgb"][0])}
     ms, sizes = {}, {}
