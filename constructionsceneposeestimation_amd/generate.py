@@ -34,7 +34,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import queue
 import sys
+import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
@@ -148,24 +150,48 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     pending = []
     t_render = 0.0
     t0 = time.time()
-    for s0 in range(0, len(frames), batch):
-        fb = frames[s0:s0 + batch]
-        epochs = sorted({f // 10 for f in fb})
-        set_of = {}
-        for k, e in enumerate(epochs):
-            st = wl.epoch(e)
-            r.set_instance_transforms(k, st.models)
-            r.set_keypoints(k, st.keypoints)
-            if st.dr is not None:
-                r.set_dr_light(k, st.dr.light)
-                r.set_dr_textures(k, st.dr.textures)
-            set_of[e] = k
+    # The GPU side runs in its own thread, one batch ahead: while the main
+    # thread builds labels and feeds the writers for batch k, batch k+1 renders
+    # (ctypes releases the GIL for the call; only this thread touches the
+    # renderer).  Output arrays are fresh per batch, so nothing is overwritten
+    # while the writers still read it.
+    batches: "queue.Queue" = queue.Queue(maxsize=2)
+
+    def produce():
+        try:
+            for s0 in range(0, len(frames), batch):
+                fb = frames[s0:s0 + batch]
+                epochs = sorted({f // 10 for f in fb})
+                set_of, states = {}, {}
+                for k, e in enumerate(epochs):
+                    st = states[e] = wl.epoch(e)
+                    r.set_instance_transforms(k, st.models)
+                    r.set_keypoints(k, st.keypoints)
+                    if st.dr is not None:
+                        r.set_dr_light(k, st.dr.light)
+                        r.set_dr_textures(k, st.dr.textures)
+                    set_of[e] = k
+                views, projs = wl.frame_params(fb)
+                tr = time.time()
+                out = r.render(make_frames(views, projs, [set_of[f // 10] for f in fb], fb), want=want)
+                batches.put((fb, states, out, time.time() - tr))
+        except BaseException as e:   # surfaced by the consumer
+            batches.put(e)
+        batches.put(None)
+
+    producer = threading.Thread(target=produce, name="csg-render", daemon=True)
+    producer.start()
+    while True:
+        item = batches.get()
+        if item is None:
+            break
+        if isinstance(item, BaseException):
+            raise item
+        fb, states, out, dt_render = item
+        t_render += dt_render
+        for e, st in states.items():
             if e not in pose_cache:
                 pose_cache[e] = object_poses(wl.scene, st.object_frames)
-        views, projs = wl.frame_params(fb)
-        tr = time.time()
-        out = r.render(make_frames(views, projs, [set_of[f // 10] for f in fb], fb), want=want)
-        t_render += time.time() - tr
         for k, f in enumerate(fb):
             V, P, C, cam, aim, q = wl.camera(f)
             lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
@@ -201,6 +227,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     for p in pending:
         _log_done(log, *p, "pointcloud" in outs)
     pool.shutdown()
+    producer.join()
     wall = time.time() - t0
     r.close()
     log.save()
