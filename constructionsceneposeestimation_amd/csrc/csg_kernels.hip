@@ -1100,6 +1100,11 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
     if ((DBG(b.dbg) & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
       atomicAdd(&b.overflow[1], 1u);
       atomicAdd(&b.overflow[2], rows);
+      const uint4 g1 = L.img.q[1][tid];
+      if (((g1.w & 0xFFFFu) - (g1.z & 0xFFFFu)) < 4u && ((g1.w >> 16) - (g1.z >> 16)) < 4u) {
+        atomicAdd(&b.overflow[9], 1u);      // records whose pixel box is at most 4 x 4
+        atomicAdd(&b.overflow[10], rows);   // ... their row items
+      }
     }
 #if CSG_L1_BITMAP
     // records with rows get compact indices; item -> record is a rank query
@@ -1157,6 +1162,9 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
       if ((DBG(b.dbg) & 512u) && w2) {      // non-empty spans, level-2 items
         atomicAdd(&b.overflow[3], 1u);
         atomicAdd(&b.overflow[4], w2);
+        const uint4 g1 = L.img.q[1][sp & 255u];
+        if (((g1.w & 0xFFFFu) - (g1.z & 0xFFFFu)) < 4u && ((g1.w >> 16) - (g1.z >> 16)) < 4u)
+          atomicAdd(&b.overflow[11], w2);   // level-2 items of records with at most 4 x 4 box
       }
 #if CSG_L2_BITMAP
       // Non-empty spans get compact indices (one packed scan gives item
