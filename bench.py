@@ -105,15 +105,18 @@ def sum_over_ranks(vals: List[int], world: int) -> List[int]:
     return [int(v) for v in t.tolist()]
 
 
-def median_time(fn: Callable[[], None], runs: int = 5, warmup: int = 1) -> float:
-    """Median wall time of ``runs`` calls after ``warmup`` untimed ones."""
+def median_time(fn: Callable[[], None], runs: int = 5, warmup: int = 1, what: str = "") -> float:
+    """Median wall time of ``runs`` calls after ``warmup`` untimed ones.
+    A progress line per call (stderr): a long CPU baseline is not silent."""
     for _ in range(warmup):
         fn()
     ts = []
-    for _ in range(runs):
+    for k in range(runs):
         t0 = time.perf_counter()
         fn()
         ts.append(time.perf_counter() - t0)
+        if what:
+            log(f"cpu baseline {what}: run {k + 1}/{runs} {ts[-1]:.2f} s")
     return statistics.median(ts)
 
 
@@ -388,9 +391,9 @@ def main():
 
             def run_all():
                 res["out"] = ver.render(sample_frames, thr)
-            t_all = median_time(run_all, runs=5, warmup=1)
+            t_all = median_time(run_all, runs=5, warmup=1, what=f"{thr} threads")
             n1 = max(1, min(args.cpu_single_frames, len(sample_frames)))
-            t_one = median_time(lambda: ver.render(sample_frames[:n1], 1), runs=5, warmup=1)
+            t_one = median_time(lambda: ver.render(sample_frames[:n1], 1), runs=5, warmup=1, what="1 thread")
             v_, p_, ref = res["out"]
             bad = ver.compare(sample_frames, v_, p_, ref, gpu_sample)
             cpu = {"value": round(len(sample_frames) / t_all, 3), "unit": "frames/s", "cores": thr, "kind": "port",
