@@ -34,54 +34,20 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import queue
 import sys
-import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
 import numpy as np
 
 from . import camera_math as cm
-from . import writers as fileio
-from .labels import label_record, object_poses, save_label_json
+from .labels import label_record, object_poses
 from .quality_log import QualityLog
-from .renderer import Renderer, make_frames
+from .renderer import Renderer, make_frames, output_spec, scene_labels
 from .shard import shard_of_range
 from .workload import Workload
-
-
-def _write_png(path: str, rgb: np.ndarray) -> None:
-    # zlib level 1 with run-length matches only: ~2x faster than the default
-    # strategy on rendered frames for ~2% more bytes (tools/gen_bench.py)
-    fileio.write_png(path, rgb, level=1, strategy="rle")
-
-
-def _write_pointcloud(path: str, points: np.ndarray, rgb: np.ndarray) -> None:
-    """``x y z r g b`` per hit pixel (generate_construction_data.py:769-770);
-    the world points come from the GPU resolve (NaN where nothing is hit)."""
-    fileio.write_pointcloud_txt(path, points, rgb)
-
-
-def _atomic(path: str, fn, *args) -> None:
-    """Write through ``path + '.tmp'`` and rename: a crash never leaves a
-    truncated file under the final name."""
-    tmp = path + ".tmp"
-    fn(tmp, *args)
-    os.replace(tmp, path)
-
-
-def _write_frame(files, label: dict, label_path: str, depth: Optional[np.ndarray] = None) -> Optional[dict]:
-    """Every file of one frame, then its label JSON: the label is the resume
-    marker (generate_construction_data.py:1357-1367 scans labels/), so it
-    appears only once the frame's other files are complete.  Returns the
-    frame's depth counts for the quality log (computed here, in the writer
-    thread, off the thread that drives the GPU)."""
-    for path, fn, args in files:
-        _atomic(path, fn, *args)
-    _atomic(label_path, lambda path, lab: save_label_json(lab, path), label)
-    return fileio.depth_stats(depth) if depth is not None else None
+from .writer_pool import WriterPool
+from .writer_pool import _write_png  # noqa: F401  (the generator's PNG settings; tools/gen_bench.py)
 
 
 def default_writers() -> int:
@@ -119,10 +85,13 @@ def parse_outputs(spec: str) -> tuple:
 def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 30,
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
-             resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None) -> dict:
+             resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
+             writer_mode: str = "process") -> dict:
     """Render ``frames`` on one GPU and write them (``outputs``, default the
     reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
-    add the depth .npy, the depth .npy + CSV, the point cloud, the normals)."""
+    add the depth .npy, the depth .npy + CSV, the point cloud, the normals).
+    ``writer_mode`` "process" encodes in worker processes fed through shared
+    memory, "thread" in threads of this process (writer_pool.py)."""
     outs = set(REFERENCE_OUTPUTS if outputs is None else outputs)
     if depth or depth_csv:
         outs.add("depth_npy")
@@ -139,102 +108,81 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         frames = [f for f in frames if not os.path.exists(os.path.join(out_dir, "labels", f"label_{f:06d}.json"))]
     host_depth = bool(outs & {"depth_csv", "depth_npy", "pointcloud"})
     log = QualityLog(os.path.join(out_dir, "logs"))
-    r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
-    intr = wl.intr
     want = (["rgb", "instance", "keypoints", "stats", "covered"] + (["depth"] if host_depth else [])
             + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
             + (["normals"] if "normals" in outs else []))
-    pose_cache = {}
     n_writers = writers or default_writers()
-    pool = ThreadPoolExecutor(max_workers=n_writers)
+    # the writer processes start here, before this process touches the GPU
+    pool = WriterPool(output_spec(batch, wl.height, wl.width, wl.n_keypoints(), scene_labels(wl.scene), want),
+                      n_writers, n_slots=3, mode=writer_mode)
+    r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
+    intr = wl.intr
+    pose_cache = {}
     pending = []
     t_render = 0.0
     t0 = time.time()
-    # The GPU side runs in its own thread, one batch ahead: while the main
-    # thread builds labels and feeds the writers for batch k, batch k+1 renders
-    # (ctypes releases the GIL for the call; only this thread touches the
-    # renderer).  Output arrays are fresh per batch, so nothing is overwritten
-    # while the writers still read it.
-    batches: "queue.Queue" = queue.Queue(maxsize=2)
-
-    def produce():
-        try:
-            for s0 in range(0, len(frames), batch):
-                fb = frames[s0:s0 + batch]
-                epochs = sorted({f // 10 for f in fb})
-                set_of, states = {}, {}
-                for k, e in enumerate(epochs):
-                    st = states[e] = wl.epoch(e)
-                    r.set_instance_transforms(k, st.models)
-                    r.set_keypoints(k, st.keypoints)
-                    if st.dr is not None:
-                        r.set_dr_light(k, st.dr.light)
-                        r.set_dr_textures(k, st.dr.textures)
-                    set_of[e] = k
-                views, projs = wl.frame_params(fb)
-                tr = time.time()
-                out = r.render(make_frames(views, projs, [set_of[f // 10] for f in fb], fb), want=want)
-                batches.put((fb, states, out, time.time() - tr))
-        except BaseException as e:   # surfaced by the consumer
-            batches.put(e)
-        batches.put(None)
-
-    producer = threading.Thread(target=produce, name="csg-render", daemon=True)
-    producer.start()
-    while True:
-        item = batches.get()
-        if item is None:
-            break
-        if isinstance(item, BaseException):
-            raise item
-        fb, states, out, dt_render = item
-        t_render += dt_render
-        for e, st in states.items():
-            if e not in pose_cache:
-                pose_cache[e] = object_poses(wl.scene, st.object_frames)
-        for k, f in enumerate(fb):
-            V, P, C, cam, aim, q = wl.camera(f)
-            lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
-                               out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
-                               wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k])
-            dk = out["depth"][k] if "depth" in out else None
-            log_args = dict(n_objects=lab["num_objects"], kp_vis=out["keypoints_vis"][k], frame_id=f, cam_pos=cam,
-                            depth_range=out["depth_range"][k] if "depth_range" in out else None)
-            files = []
-            if "rgb" in outs:
-                files.append((os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), _write_png, (out["rgb"][k],)))
-            if "mask" in outs:
-                files.append((os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"), fileio.write_npy,
-                              (out["instance"][k],)))
-            if "depth_npy" in outs:
-                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"), fileio.write_npy, (dk,)))
-            if "depth_csv" in outs:
-                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), fileio.write_depth_csv, (dk,)))
-            if "depth_png" in outs:
-                files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.png"), _write_png,
-                              (out["depth_vis"][k],)))
-            if "pointcloud" in outs:
-                files.append((os.path.join(out_dir, "pointcloud", f"pointcloud_{f:06d}.txt"), _write_pointcloud,
-                              (out["points"][k], out["rgb"][k])))
-            if "normals" in outs:
-                files.append((os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), fileio.write_npy,
-                              (out["normals"][k],)))
-            fut = pool.submit(_write_frame, files, lab, os.path.join(out_dir, "labels", f"label_{f:06d}.json"), dk)
-            pending.append((fut, log_args))
-        # bound the queue so host memory stays flat; log frames in order as they complete
-        while len(pending) > 4 * n_writers:
-            _log_done(log, *pending.pop(0), "pointcloud" in outs)
-    for p in pending:
-        _log_done(log, *p, "pointcloud" in outs)
-    pool.shutdown()
-    producer.join()
+    try:
+        for b, s0 in enumerate(range(0, len(frames), batch)):
+            fb = frames[s0:s0 + batch]
+            slot = b % pool.n_slots
+            arrays = pool.arrays(slot)          # (waits until the writers are done with the slot)
+            epochs = sorted({f // 10 for f in fb})
+            set_of = {}
+            for k, e in enumerate(epochs):
+                st = wl.epoch(e)
+                r.set_instance_transforms(k, st.models)
+                r.set_keypoints(k, st.keypoints)
+                if st.dr is not None:
+                    r.set_dr_light(k, st.dr.light)
+                    r.set_dr_textures(k, st.dr.textures)
+                set_of[e] = k
+                if e not in pose_cache:
+                    pose_cache[e] = object_poses(wl.scene, st.object_frames)
+            views, projs = wl.frame_params(fb)
+            tr = time.time()
+            out = r.render(make_frames(views, projs, [set_of[f // 10] for f in fb], fb), want=want,
+                           out={k: v[:len(fb)] for k, v in arrays.items()})
+            t_render += time.time() - tr
+            for k, f in enumerate(fb):
+                V, P, C, cam, aim, q = wl.camera(f)
+                lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
+                                   out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
+                                   wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k])
+                log_args = dict(n_objects=lab["num_objects"], kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
+                                cam_pos=cam, depth_range=out["depth_range"][k].copy() if "depth_range" in out else None)
+                files = []
+                if "rgb" in outs:
+                    files.append((os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), "png", ("rgb",)))
+                if "mask" in outs:
+                    files.append((os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"), "npy", ("instance",)))
+                if "depth_npy" in outs:
+                    files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"), "npy", ("depth",)))
+                if "depth_csv" in outs:
+                    files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), "csv", ("depth",)))
+                if "depth_png" in outs:
+                    files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.png"), "png", ("depth_vis",)))
+                if "pointcloud" in outs:
+                    files.append((os.path.join(out_dir, "pointcloud", f"pointcloud_{f:06d}.txt"), "pointcloud",
+                                  ("points", "rgb")))
+                if "normals" in outs:
+                    files.append((os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), "npy", ("normals",)))
+                fut = pool.submit(slot, k, files, lab, os.path.join(out_dir, "labels", f"label_{f:06d}.json"))
+                pending.append((fut, log_args))
+            del out, arrays
+            # log frames in order as they complete
+            while pending and pending[0][0].done():
+                _log_done(log, *pending.pop(0), "pointcloud" in outs)
+        for p in pending:
+            _log_done(log, *p, "pointcloud" in outs)
+    finally:
+        pool.close()
+        r.close()
     wall = time.time() - t0
-    r.close()
     log.save()
     summary = log.summary()
     summary["throughput"] = {"frames": len(frames), "wall_s": round(wall, 3), "render_s": round(t_render, 3),
                              "frames_per_s": round(len(frames) / wall, 2) if wall > 0 else None,
-                             "writers": n_writers, "outputs": sorted(outs)}
+                             "writers": n_writers, "writer_mode": writer_mode, "outputs": sorted(outs)}
     return summary
 
 
@@ -256,14 +204,15 @@ def main(argv=None):
     ap.add_argument("--depth-csv", action="store_true", help="add depth .npy and CSV")
     ap.add_argument("--pointcloud", action="store_true")
     ap.add_argument("--normals", action="store_true")
-    ap.add_argument("--writers", type=int, default=0, help="writer threads (0: the CPUs this process may use)")
+    ap.add_argument("--writers", type=int, default=0, help="writer processes (0: the CPUs this process may use)")
+    ap.add_argument("--writer-mode", default="process", choices=("process", "thread"))
     ap.add_argument("--no-resume", action="store_true")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
                        a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
-                       outputs=parse_outputs(a.outputs))
+                       outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode)
     print(json.dumps(summary))
 
 

@@ -47,6 +47,39 @@ def _light_struct(light) -> "_lib.Light":
     return L
 
 
+def scene_labels(scene: Scene) -> int:
+    """Label-table length of a scene (the renderers' ``n_labels``)."""
+    n = max([o.inst_idx for o in scene.objects] + [i.inst_idx for i in scene.instances] + [-1]) + 1
+    return max(n, 1)
+
+
+def output_spec(n: int, H: int, W: int, n_kp: int, n_labels: int, want: Iterable[str]) -> Dict[str, tuple]:
+    """Host arrays a render of ``n`` frames fills for ``want``: name -> (shape, dtype)."""
+    want = set(want)
+    spec: Dict[str, tuple] = {}
+    if "rgb" in want:
+        spec["rgb"] = ((n, H, W, 3), np.uint8)
+    if "instance" in want:
+        spec["instance"] = ((n, H, W), np.int32)
+    if "depth" in want:
+        spec["depth"] = ((n, H, W), np.float32)
+    if "keypoints" in want and n_kp:
+        spec["keypoints_uv"] = ((n, n_kp, 2), np.float32)
+        spec["keypoints_vis"] = ((n, n_kp), np.int32)
+    if "stats" in want:
+        spec["inst_stats"] = ((n, n_labels, 5), np.uint32)
+    if "normals" in want:
+        spec["normals"] = ((n, H, W, 3), np.float16)
+    if "points" in want:
+        spec["points"] = ((n, H, W, 3), np.float32)
+    if "depth_vis" in want:   # the reference's JET depth PNG (GDP:1690-1709) and its min / max
+        spec["depth_vis"] = ((n, H, W, 3), np.uint8)
+        spec["depth_range"] = ((n, 2), np.float32)
+    if "covered" in want:     # unoccluded pixels per label (occlusionRatio)
+        spec["label_covered"] = ((n, n_labels), np.uint32)
+    return spec
+
+
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, max_frames: int = 8, device: int = 0,
                  intrinsics: Optional[Intrinsics] = None, records_per_frame: int = 0, bins_per_frame: int = 0,
@@ -66,6 +99,7 @@ class Renderer:
         self.packed: PackedScene = pack_scene(scene)
         self.n_inst = len(scene.instances)
         self.n_labels = max(self.packed.n_labels, 1)
+        assert self.n_labels == scene_labels(scene)
         self.n_kp = 0
         self._upload()
 
@@ -152,33 +186,26 @@ class Renderer:
         self.n_kp = p.shape[0]
 
     # -- rendering ------------------------------------------------------------
-    def render(self, frames: np.ndarray, want: Iterable[str] = ("rgb", "instance", "depth")) -> Dict[str, np.ndarray]:
-        """Render a batch to host numpy arrays (synchronous; includes D2H copies)."""
-        want = set(want)
+    def output_spec(self, n: int, want: Iterable[str]) -> Dict[str, tuple]:
+        """Host arrays :meth:`render` fills for ``want``: name -> (shape, dtype)."""
+        return output_spec(n, self.height, self.width, self.n_kp, self.n_labels, want)
+
+    def render(self, frames: np.ndarray, want: Iterable[str] = ("rgb", "instance", "depth"),
+               out: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
+        """Render a batch to host numpy arrays (synchronous; includes D2H copies).
+        ``out`` supplies the arrays (e.g. views of shared memory), shaped as
+        :meth:`output_spec` says; otherwise they are allocated."""
         frames = np.ascontiguousarray(frames, FRAME_DTYPE)
         n = frames.shape[0]
-        H, W = self.height, self.width
-        out: Dict[str, np.ndarray] = {}
-        if "rgb" in want:
-            out["rgb"] = np.empty((n, H, W, 3), np.uint8)
-        if "instance" in want:
-            out["instance"] = np.empty((n, H, W), np.int32)
-        if "depth" in want:
-            out["depth"] = np.empty((n, H, W), np.float32)
-        if "keypoints" in want and self.n_kp:
-            out["keypoints_uv"] = np.empty((n, self.n_kp, 2), np.float32)
-            out["keypoints_vis"] = np.empty((n, self.n_kp), np.int32)
-        if "stats" in want:
-            out["inst_stats"] = np.empty((n, self.n_labels, 5), np.uint32)
-        if "normals" in want:
-            out["normals"] = np.empty((n, H, W, 3), np.float16)
-        if "points" in want:
-            out["points"] = np.empty((n, H, W, 3), np.float32)
-        if "depth_vis" in want:   # the reference's JET depth PNG (GDP:1690-1709) and its min / max
-            out["depth_vis"] = np.empty((n, H, W, 3), np.uint8)
-            out["depth_range"] = np.empty((n, 2), np.float32)
-        if "covered" in want:     # unoccluded pixels per label (occlusionRatio)
-            out["label_covered"] = np.empty((n, self.n_labels), np.uint32)
+        spec = self.output_spec(n, want)
+        if out is None:
+            out = {k: np.empty(shape, dt) for k, (shape, dt) in spec.items()}
+        else:
+            for k, (shape, dt) in spec.items():
+                a = out.get(k)
+                if a is None or a.shape != shape or a.dtype != dt or not a.flags.c_contiguous:
+                    raise CsgError(f"render: out[{k!r}] must be a C-contiguous {np.dtype(dt)} array of shape {shape}")
+            out = {k: out[k] for k in spec}
         for s in range(0, n, self.max_frames):
             e = min(n, s + self.max_frames)
             oo = _lib.Outputs()

@@ -1,0 +1,160 @@
+"""Writer pool of the generator: frames rendered on the GPU are encoded and
+written to disk by worker processes (or threads), the role of the
+reference's per-frame cv2.imwrite / np.save / np.savetxt / json.dump calls
+(generate_construction_data.py:1668-1711, :2055-2072), run in parallel with
+the GPU.
+
+Why processes: a frame's files are encoded by the native writers
+(libcsgio.so, GIL released), but its label JSON (``json.dump(indent=2)``,
+about 80 KB with keypoints) is pure Python and holds the GIL for ~4 ms, so
+one process's writer threads cap the rate near 160 frames/s at 1080p
+(profiles/r02/generate_C3_1080p_reference_outputs.json).  Worker processes
+have a GIL each.
+
+Frames reach the workers through shared memory: the renderer writes each
+batch's outputs straight into one slot of a ring of ``n_slots`` shared
+batch buffers (:meth:`Renderer.render` ``out=``), a task names (slot, frame)
+plus the frame's small label dict, and a slot is reused only after every
+task that reads it has finished.  The processes are spawned before the
+parent touches the GPU and never use it.
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+from concurrent.futures import Future, ProcessPoolExecutor, ThreadPoolExecutor
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+Layout = Dict[str, Tuple[int, tuple, str]]     # name -> (byte offset in a slot, shape, dtype)
+
+
+def _atomic(path: str, fn, *args) -> None:
+    """Write through ``path + '.tmp'`` and rename: a crash never leaves a
+    truncated file under the final name."""
+    tmp = path + ".tmp"
+    fn(tmp, *args)
+    os.replace(tmp, path)
+
+
+def _write_png(path: str, rgb: np.ndarray) -> None:
+    from . import writers as fileio
+    # zlib level 1 with run-length matches only: ~2x faster than the default
+    # strategy on rendered frames for ~2% more bytes (tools/gen_bench.py)
+    fileio.write_png(path, rgb, level=1, strategy="rle")
+
+
+def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, str, Tuple[str, ...]]],
+                label: dict, label_path: str) -> Optional[dict]:
+    """Every file of frame ``k`` of a batch, then its label JSON (the resume
+    marker, GDP:1357-1367 scans labels/).  ``files`` = (path, kind, array
+    names); returns the frame's depth counts for the quality log."""
+    from . import writers as fileio
+    from .labels import save_label_json
+    for path, kind, keys in files:
+        a = [arrays[x][k] for x in keys]
+        if kind == "png":
+            _atomic(path, _write_png, *a)
+        elif kind == "npy":
+            _atomic(path, fileio.write_npy, *a)
+        elif kind == "csv":
+            _atomic(path, fileio.write_depth_csv, *a)
+        elif kind == "pointcloud":
+            _atomic(path, fileio.write_pointcloud_txt, *a)
+        else:
+            raise ValueError(kind)
+    _atomic(label_path, lambda p, lab: save_label_json(lab, p), label)
+    return fileio.depth_stats(arrays["depth"][k]) if "depth" in arrays else None
+
+
+# -- worker-process side ---------------------------------------------------------
+_ATTACHED: Dict[str, object] = {}
+
+
+def _views(shm_name: str, slot_bytes: int, layout: Layout, slot: int) -> Dict[str, np.ndarray]:
+    from multiprocessing import resource_tracker, shared_memory
+    shm = _ATTACHED.get(shm_name)
+    if shm is None:
+        shm = shared_memory.SharedMemory(name=shm_name)
+        # the parent owns the segment: this process must not unlink it at exit
+        resource_tracker.unregister(shm._name, "shared_memory")   # noqa: SLF001
+        _ATTACHED[shm_name] = shm
+    base = slot * slot_bytes
+    return {k: np.ndarray(shape, np.dtype(dt), buffer=shm.buf, offset=base + off)
+            for k, (off, shape, dt) in layout.items()}
+
+
+def _task(shm_name, slot_bytes, layout, slot, k, files, label, label_path):
+    return write_frame(_views(shm_name, slot_bytes, layout, slot), k, files, label, label_path)
+
+
+def _ping() -> int:
+    return os.getpid()
+
+
+# -- parent side -----------------------------------------------------------------
+class WriterPool:
+    """``n_slots`` batch buffers shaped by ``spec`` (name -> (shape, dtype) of
+    one batch, Renderer.output_spec) and ``workers`` writer processes (mode
+    "process") or threads (mode "thread")."""
+
+    def __init__(self, spec: Dict[str, tuple], workers: int, n_slots: int = 3, mode: str = "process"):
+        self.mode = mode
+        self.layout: Layout = {}
+        off = 0
+        for k, (shape, dt) in spec.items():
+            off = (off + 255) & ~255
+            self.layout[k] = (off, tuple(int(x) for x in shape), np.dtype(dt).str)
+            off += int(np.prod(shape)) * np.dtype(dt).itemsize
+        self.slot_bytes = (off + 4095) & ~4095
+        self.n_slots = n_slots
+        self.busy: List[List[Future]] = [[] for _ in range(n_slots)]
+        self.shm = None
+        if mode == "process":
+            from multiprocessing import shared_memory
+            self.shm = shared_memory.SharedMemory(create=True, size=max(self.slot_bytes * n_slots, 1))
+            self.pool = ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn"))
+            # start every worker now, before the parent initialises the GPU
+            for f in [self.pool.submit(_ping) for _ in range(workers)]:
+                f.result()
+            self._local = None
+        elif mode == "thread":
+            self.pool = ThreadPoolExecutor(max_workers=workers)
+            self._local = [{k: np.empty(shape, np.dtype(dt)) for k, (_, shape, dt) in self.layout.items()}
+                           for _ in range(n_slots)]
+        else:
+            raise ValueError(f"writer mode {mode!r}: 'process' or 'thread'")
+
+    def arrays(self, slot: int) -> Dict[str, np.ndarray]:
+        """The slot's arrays, to render into (waits until no task reads it)."""
+        for f in self.busy[slot]:
+            f.result()
+        self.busy[slot] = []
+        if self.shm is not None:
+            base = slot * self.slot_bytes
+            return {k: np.ndarray(shape, np.dtype(dt), buffer=self.shm.buf, offset=base + off)
+                    for k, (off, shape, dt) in self.layout.items()}
+        return self._local[slot]
+
+    def submit(self, slot: int, k: int, files, label: dict, label_path: str) -> Future:
+        if self.shm is not None:
+            f = self.pool.submit(_task, self.shm.name, self.slot_bytes, self.layout, slot, k, files, label,
+                                 label_path)
+        else:
+            f = self.pool.submit(write_frame, self._local[slot], k, files, label, label_path)
+        self.busy[slot].append(f)
+        return f
+
+    def close(self) -> None:
+        for fs in self.busy:
+            for f in fs:
+                f.result()
+        self.pool.shutdown()
+        if self.shm is not None:
+            try:
+                self.shm.close()
+            except BufferError:   # a caller still holds a view of a slot: the mapping goes with it
+                pass
+            self.shm.unlink()
+            self.shm = None
