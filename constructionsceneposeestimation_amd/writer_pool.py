@@ -4,12 +4,14 @@ reference's per-frame cv2.imwrite / np.save / np.savetxt / json.dump calls
 (generate_construction_data.py:1668-1711, :2055-2072), run in parallel with
 the GPU.
 
-Why processes: a frame's files are encoded by the native writers
-(libcsgio.so, GIL released), but its label JSON (``json.dump(indent=2)``,
-about 80 KB with keypoints) is pure Python and holds the GIL for ~4 ms, so
-one process's writer threads cap the rate near 160 frames/s at 1080p
-(profiles/r02/generate_C3_1080p_reference_outputs.json).  Worker processes
-have a GIL each.
+Threads (the default) or processes: a frame's files are encoded by the
+native writers (libcsgio.so, GIL released), but its label JSON
+(``json.dump(indent=2)``, about 80 KB with keypoints) is pure Python and
+holds the GIL for ~4 ms.  Worker processes have a GIL each; measured on C3
+at 1080p with 16 writers they are nevertheless slower (184 vs 233 frames/s:
+every worker page-faults the shared slots it reads, and each task is
+pickled), so threads are the default and processes an option for heavier
+per-frame Python work.
 
 Frames reach the workers through shared memory: the renderer writes each
 batch's outputs straight into one slot of a ring of ``n_slots`` shared
@@ -73,12 +75,12 @@ _ATTACHED: Dict[str, object] = {}
 
 
 def _views(shm_name: str, slot_bytes: int, layout: Layout, slot: int) -> Dict[str, np.ndarray]:
-    from multiprocessing import resource_tracker, shared_memory
+    from multiprocessing import shared_memory
     shm = _ATTACHED.get(shm_name)
     if shm is None:
+        # (attaching registers the name with the parent's resource tracker
+        # again, a no-op: the parent unlinks it and unregisters it once)
         shm = shared_memory.SharedMemory(name=shm_name)
-        # the parent owns the segment: this process must not unlink it at exit
-        resource_tracker.unregister(shm._name, "shared_memory")   # noqa: SLF001
         _ATTACHED[shm_name] = shm
     base = slot * slot_bytes
     return {k: np.ndarray(shape, np.dtype(dt), buffer=shm.buf, offset=base + off)
