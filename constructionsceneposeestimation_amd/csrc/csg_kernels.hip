@@ -58,6 +58,9 @@ namespace csg {
 #ifndef CSG_ALPHA_CLASS
 #define CSG_ALPHA_CLASS 1      // alpha tests decided by the 2-bit quad class where it can (see alpha_pass)
 #endif
+#ifndef CSG_SETUP_TRANSPOSE
+#define CSG_SETUP_TRANSPOSE 1  // k_setup stores each wave's records as consecutive 16-B chunks via LDS
+#endif
 #ifndef CSG_SMALL_COVER
 #define CSG_SMALL_COVER 4      // records with at most N x N pixel centres get an exact cover test in k_setup (0: off)
 #endif
@@ -616,6 +619,47 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   uint32_t wbase = 0;
   if (lane == 0 && wtot) wbase = atomicAdd(&b.rec_count[f * kCounterStride], wtot);
   wbase = __shfl(wbase, 0, 64);
+  if (DBG(b.dbg) & 128u) {   // ablation: no record stores
+    if (nrec == 3 && b.inst) b.inst[0] = r0.uid + r1.uid;
+    return;
+  }
+#if CSG_SETUP_TRANSPOSE
+  // Coalesced record stores.  The wave's records take the contiguous slots
+  // [wbase, wbase + wtot), but lane-by-lane 16-B stores at a 112-B stride
+  // write ~7x more partial 128-B lines than the bytes need.  So, 16 records
+  // at a time, the lanes holding them put them in a per-wave LDS stage and the
+  // wave stores the stage as consecutive 16-B chunks (1 KB per instruction).
+  // Wave-local: the loop count is uniform per wave, so there is no block barrier.
+  __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
+  uint4* sw = tstage[tid >> 6];
+  if (lane == 0 && wbase + wtot > b.rec_cap) atomicOr(b.overflow, 1u);
+  uint4* dst = reinterpret_cast<uint4*>(b.recs + (size_t)f * b.rec_cap);
+  const size_t lim = (size_t)b.rec_cap * kRecGroups;
+  uint4 q0[kRecGroups], q1[kRecGroups];
+  __builtin_memcpy(q0, &r0, sizeof(Rec));
+  __builtin_memcpy(q1, &r1, sizeof(Rec));
+  for (uint32_t p0 = 0; p0 < wtot; p0 += 16) {
+    if (nrec > 0 && mine - p0 < 16u) {
+#pragma unroll
+      for (int k = 0; k < kRecGroups; ++k) sw[(mine - p0) * kRecGroups + k] = q0[k];
+    }
+    if (nrec > 1 && mine + 1u - p0 < 16u) {
+#pragma unroll
+      for (int k = 0; k < kRecGroups; ++k) sw[(mine + 1u - p0) * kRecGroups + k] = q1[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nch = min(16u, wtot - p0) * kRecGroups;
+    const size_t at = ((size_t)wbase + p0) * kRecGroups;
+#pragma unroll
+    for (uint32_t c = (uint32_t)lane; c < 2u * 64u; c += 64u)
+      if (c < nch && at + c < lim) dst[at + c] = sw[c];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (nrec > 0 && wbase + mine < b.rec_cap) b.rect[(size_t)f * b.rec_cap + wbase + mine] = rec_tile_rect(r0);
+  if (nrec > 1 && wbase + mine + 1 < b.rec_cap) b.rect[(size_t)f * b.rec_cap + wbase + mine + 1] = rec_tile_rect(r1);
+#else
   auto emit = [&](const Rec& rec, uint32_t slot) {
     if (slot >= b.rec_cap) {
       atomicOr(b.overflow, 1u);
@@ -624,12 +668,9 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     store_rec(b.recs + (size_t)f * b.rec_cap + slot, rec);
     b.rect[(size_t)f * b.rec_cap + slot] = rec_tile_rect(rec);
   };
-  if (DBG(b.dbg) & 128u) {   // ablation: no record stores
-    if (nrec == 3 && b.inst) b.inst[0] = r0.uid + r1.uid;
-    return;
-  }
   if (nrec > 0) emit(r0, wbase + mine);
   if (nrec > 1) emit(r1, wbase + mine + 1);
+#endif
 }
 
 // ---------------------------------------------------------------------------
