@@ -140,8 +140,9 @@ def roofline(b_geom: int, b_tex: int, b_out: int, frames_per_launch: float, rast
     kernels = [
         kern("k_raster", round(frames_per_launch * (b_tex + b_out)), raster_ms,
              "B_out + B_tex: outputs written once, bound textures read once"),
-        kern("k_setup", round(frames_per_launch * (b_geom + records_per_frame * RECORD_BYTES)), setup_ms,
-             "B_geom + raster records: authored geometry read once, 116 B written per record (k_clip + k_setup)"),
+        kern("k_setup", round(b_geom + frames_per_launch * records_per_frame * RECORD_BYTES), setup_ms,
+             "B_geom once per launch (the launch's frames share the geometry through L2 and the Infinity "
+             "Cache: the grid runs frame-fast) + 116 B written per raster record (k_clip + k_setup)"),
     ]
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic.get("k_raster"), "kernel": "k_raster",

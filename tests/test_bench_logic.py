@@ -54,7 +54,7 @@ def test_roofline_formula_follows_survey_8d():
     assert r["traffic"] == 99 and r["bound"] == "hbm" and r["unit"] == "GB/s"
     ks = {k["kernel"]: k for k in r["kernels"]}
     assert ks["k_raster"]["bytes_per_launch"] == 10 * (200 + 300) * M
-    assert ks["k_setup"]["bytes_per_launch"] == 10 * (1000 + 5 * bench.RECORD_BYTES) * M
+    assert ks["k_setup"]["bytes_per_launch"] == (1000 + 10 * 5 * bench.RECORD_BYTES) * M   # geometry once per launch
     assert r["frame_level"]["frac"] == pytest.approx(1000.0 * b_frame / (bench.HBM_PEAK_GBS * 1e9), rel=1e-3)
 
 
