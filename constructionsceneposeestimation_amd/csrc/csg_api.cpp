@@ -645,6 +645,7 @@ static int ensure_work(csg_ctx* c) {
     c->rec_cap = c->cfg.records_per_frame ? c->cfg.records_per_frame
                                           : (uint32_t)std::min<uint64_t>(c->n_tris_total + c->n_tris_total / 8 + 4096,
                                                                          0x7FFFFFFFull);
+  c->rec_cap = (c->rec_cap + 3u) & ~3u;   // 16-B aligned rect rows per frame (k_count / k_bin load 4 at once)
   if (!c->bin_cap)
     c->bin_cap = c->cfg.bins_per_frame ? c->cfg.bins_per_frame
                                        : (uint32_t)std::min<uint64_t>(3ull * c->rec_cap + 16ull * c->n_tiles,
@@ -930,7 +931,7 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
     auto grow = [](uint32_t cap, uint32_t need) {
       return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * cap, need + need / 8ull + 1024ull), 0x7FFFFFFFull);
     };
-    if (ov & kOvRecords) c->rec_cap = grow(c->rec_cap, need_rec);
+    if (ov & kOvRecords) c->rec_cap = (grow(c->rec_cap, need_rec) + 3u) & ~3u;
     if (ov & kOvBins) c->bin_cap = grow(c->bin_cap, need_bin);
     if (ov & kOvRecords) c->bin_cap = grow(c->bin_cap, 0);   // more records: more bin entries too
     c->work_frames = 0;

@@ -674,35 +674,92 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
 }
 
 // ---------------------------------------------------------------------------
+// Binning rounds.  A round takes kBinRpt records per thread (kBinRound per
+// block, each thread's records consecutive: one 16-B load of their tile
+// rects), scans their tile counts into pre[] and expands (record, tile) items
+// with a 4-ary search.  Bigger rounds mean fewer barriers, tile sweeps and --
+// in k_bin -- fewer rounds of latency-bound global reservations per block.
+// ---------------------------------------------------------------------------
+#ifndef CSG_BIN_RPT
+#define CSG_BIN_RPT 4
+#endif
+constexpr int kBinRpt = CSG_BIN_RPT;
+constexpr uint32_t kBinRound = kBlock * kBinRpt;
+static_assert(kBinRpt == 1 || kBinRpt == 4, "records per thread per binning round");
+
+// last k in [0, kBinRound) with pre[k] <= j (pre: kBinRound + 1 entries, nondecreasing)
+__device__ __forceinline__ int find_bin_item(const uint32_t* pre, uint32_t j) {
+  if constexpr (kBinRpt == 1) {
+    return find_item(pre, j);
+  } else {
+    int lo = 0;
+#pragma unroll
+    for (int step = 256; step > 0; step >>= 2) {
+      const uint32_t a = pre[lo + step], b2 = pre[lo + 2 * step], c = pre[lo + 3 * step];
+      lo += ((a <= j) + (b2 <= j) + (c <= j)) * step;
+    }
+    return lo;
+  }
+}
+
+// Load this thread's records of the round at `base` (record ids base + tid*kBinRpt + q),
+// fill lrc[] and pre[]; returns the round's item total.
+__device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32_t base, uint32_t n, uint32_t* lrc,
+                                                    uint32_t* pre, uint32_t* wsum) {
+  const int tid = threadIdx.x;
+  const uint32_t r0 = base + (uint32_t)tid * kBinRpt;
+  uint32_t rc[kBinRpt], area[kBinRpt], sum = 0;
+  if constexpr (kBinRpt == 4) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r0 + 3 < n) {
+      v = *reinterpret_cast<const uint4*>(rect + r0);   // rect rows are 16-B aligned (rec_cap % 4 == 0)
+    } else {
+      if (r0 < n) v.x = rect[r0];
+      if (r0 + 1 < n) v.y = rect[r0 + 1];
+      if (r0 + 2 < n) v.z = rect[r0 + 2];
+    }
+    rc[0] = v.x; rc[1] = v.y; rc[2] = v.z; rc[3] = v.w;
+  } else {
+    rc[0] = r0 < n ? rect[r0] : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < kBinRpt; ++q) {
+    area[q] = (r0 + (uint32_t)q < n) ? rect_area(rc[q]) : 0u;
+    lrc[tid * kBinRpt + q] = rc[q];
+  }
+#pragma unroll
+  for (int q = 0; q < kBinRpt; ++q) sum += area[q];
+  uint32_t total;
+  uint32_t ex = block_excl_scan(sum, wsum, total);
+#pragma unroll
+  for (int q = 0; q < kBinRpt; ++q) {
+    pre[tid * kBinRpt + q] = ex;
+    ex += area[q];
+  }
+  if (tid == kBlock - 1) pre[kBinRound] = ex;
+  return total;
+}
+
+// ---------------------------------------------------------------------------
 // k_count: per-tile record counts (LDS-aggregated, grid-stride over a frame's records)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn_count[];
   uint32_t* hist = dyn_count;                          // [n_tiles]
-  uint32_t* pre = dyn_count + ((s.n_tiles + 3u) & ~3u);   // [kBlock + 1]
-  uint32_t* lrc = pre + kBlock + 4;                    // [kBlock]
-  uint32_t* wsum = lrc + kBlock;                       // [4]
+  uint32_t* pre = dyn_count + ((s.n_tiles + 3u) & ~3u);   // [kBinRound + 1]
+  uint32_t* lrc = pre + kBinRound + 4;                 // [kBinRound]
+  uint32_t* wsum = lrc + kBinRound;                    // [4]
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x;
   const uint32_t n = min(b.rec_count[f * kCounterStride], b.rec_cap);
   const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
   __syncthreads();
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-    const uint32_t r = base + tid;
-    uint32_t area = 0;
-    if (r < n) {
-      const uint32_t rc = rect[r];
-      lrc[tid] = rc;
-      area = rect_area(rc);
-    }
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(area, wsum, total);
-    pre[tid] = ex;
-    if (tid == kBlock - 1) pre[kBlock] = ex + area;
+  for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
+    const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_item(pre, j);
+      const int k = find_bin_item(pre, j);
       atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
     }
     __syncthreads();
@@ -749,8 +806,8 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   extern __shared__ uint32_t dyn[];
   uint32_t* hist = dyn;                  // [n_tiles]
   uint32_t* tbase = dyn + s.n_tiles;     // [n_tiles]
-  __shared__ uint32_t pre[kBlock + 1];
-  __shared__ uint32_t lrc[kBlock];
+  __shared__ uint32_t pre[kBinRound + 1];
+  __shared__ uint32_t lrc[kBinRound];
   __shared__ uint32_t wsum[kBlock / 64];
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x;
@@ -761,21 +818,11 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
   __syncthreads();
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-    const uint32_t r = base + tid;
-    uint32_t area = 0;
-    if (r < n) {
-      const uint32_t rc = rect[r];
-      lrc[tid] = rc;
-      area = rect_area(rc);
-    }
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(area, wsum, total);
-    pre[tid] = ex;
-    if (tid == kBlock - 1) pre[kBlock] = ex + area;
+  for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
+    const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_item(pre, j);
+      const int k = find_bin_item(pre, j);
       atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
     }
     __syncthreads();
@@ -788,7 +835,7 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
     }
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_item(pre, j);
+      const int k = find_bin_item(pre, j);
       const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
       const uint32_t slot = tbase[t] + atomicAdd(&hist[t], 1u);
       if (slot < b.bin_cap) bins[slot] = base + (uint32_t)k;
@@ -2033,7 +2080,7 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
 }
 
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
-  const size_t lds = (((s.n_tiles + 3u) & ~3u) + 3 * kBlock + 12) * sizeof(uint32_t);
+  const size_t lds = (((s.n_tiles + 3u) & ~3u) + 2 * kBinRound + 12) * sizeof(uint32_t);
   hipLaunchKernelGGL(k_count, dim3(blocks, F), dim3(kBlock), lds, st, s, b);
 }
 
