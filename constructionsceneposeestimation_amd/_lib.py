@@ -12,16 +12,19 @@ from typing import Optional
 PKG = os.path.dirname(os.path.abspath(__file__))
 # CSG_LIB names an alternative build of the same ABI (A/B timing of kernel variants)
 LIB_PATH = os.environ.get("CSG_LIB") or os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 7  # CSG_ABI_VERSION in include/csg_api.h
+ABI_VERSION = 8  # CSG_ABI_VERSION in include/csg_api.h
 KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
 COVERED_UNKNOWN = 0x80000000  # csg_outputs.label_covered flag: a tile held more than 32 labels
+ERR_CAPACITY = -6  # CSG_ERR_CAPACITY
+# csg_outputs.file_kinds (CSG_FILE_*): files encoded on the GPU, one per kind per frame, in bit order
+FILE_KINDS = {"rgb_png": 1, "depth_csv": 2, "depth_png": 4}
 
 EXPORTED = (
     "csg_create", "csg_destroy", "csg_last_error", "csg_abi_version", "csg_upload_scene",
     "csg_upload_texture", "csg_set_light", "csg_set_instance_transforms", "csg_set_keypoints",
     "csg_render_batch", "csg_render_batch_async", "csg_synchronize", "csg_get_batch_stats",
     "csg_project_keypoints", "csg_timing_reset", "csg_timing_read", "csg_set_dr_light", "csg_set_dr_textures",
-    "csg_instance_bounds",
+    "csg_instance_bounds", "csg_copy_files", "csg_host_alloc", "csg_host_free",
 )
 
 
@@ -67,7 +70,8 @@ class Outputs(C.Structure):
                 ("keypoints_uv", C.c_void_p), ("keypoints_vis", C.c_void_p), ("inst_stats", C.c_void_p),
                 ("n_labels", C.c_uint32), ("on_device", C.c_int32), ("normals", C.c_void_p),
                 ("points", C.c_void_p), ("depth_vis", C.c_void_p), ("depth_range", C.c_void_p),
-                ("label_covered", C.c_void_p)]
+                ("label_covered", C.c_void_p), ("file_kinds", C.c_uint32), ("pad_files", C.c_uint32),
+                ("files", C.c_void_p), ("files_cap", C.c_uint64), ("file_offsets", C.c_void_p)]
 
 
 class BatchStats(C.Structure):
@@ -138,6 +142,9 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib.csg_project_keypoints.argtypes = [vp, vp, u32, vp, vp, vp, vp]
     lib.csg_timing_reset.argtypes = [vp]
     lib.csg_timing_read.argtypes = [vp, C.POINTER(Timing)]
+    lib.csg_copy_files.argtypes = [vp, vp, C.c_uint64, vp]
+    lib.csg_host_alloc.argtypes = [vp, C.c_uint64, C.POINTER(vp)]
+    lib.csg_host_free.argtypes = [vp, vp]
     lib.csg_set_dr_light.argtypes = [vp, u32, C.POINTER(Light)]
     lib.csg_set_dr_textures.argtypes = [vp, u32, vp, u32]
     lib.csg_instance_bounds.argtypes = [vp, u32, vp]

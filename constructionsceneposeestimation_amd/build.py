@@ -15,8 +15,10 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libcsg.so")
-SOURCES = [os.path.join(PKG, "csrc", "csg_kernels.hip"), os.path.join(PKG, "csrc", "csg_api.cpp")]
-DEPS = SOURCES + [os.path.join(PKG, "csrc", "csg_kernels.h"), os.path.join(ROOT, "include", "csg_api.h")]
+SOURCES = [os.path.join(PKG, "csrc", "csg_kernels.hip"), os.path.join(PKG, "csrc", "csg_encode.hip"),
+           os.path.join(PKG, "csrc", "csg_api.cpp")]
+DEPS = SOURCES + [os.path.join(PKG, "csrc", "csg_kernels.h"), os.path.join(PKG, "csrc", "csg_encode.h"),
+                  os.path.join(PKG, "csrc", "csg_deflate.h"), os.path.join(ROOT, "include", "csg_api.h")]
 ARCH = os.environ.get("CSG_OFFLOAD_ARCH", "gfx950")
 IO_LIB = os.path.join(PKG, "libcsgio.so")
 IO_SOURCES = [os.path.join(PKG, "csrc", "csg_io.cpp")]

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/csg_api.h"
+#include "csg_encode.h"
 #include "csg_kernels.h"
 
 using namespace csg;
@@ -137,6 +138,18 @@ struct csg_ctx {
   DevBuf<uint32_t> o_cov;               // label coverage (host-output mode)
   DevBuf<uint32_t> drange;              // [2][chain frames] min / max depth bits (k_depth_range)
   DevBuf<uint32_t> jet;                 // JET colour map, 256 x (r | g << 8 | b << 16)
+  // images of the last batch (for the file encoders) and the encoders' buffers
+  const uint8_t* last_rgb = nullptr;
+  const float* last_depth = nullptr;
+  const uint8_t* last_dvis = nullptr;
+  DevBuf<EncPng> enc_rgb, enc_dpng;
+  DevBuf<uint2> enc_rowsum;
+  DevBuf<uint32_t> enc_rows_rgb, enc_rows_dpng, enc_rows_csv;
+  DevBuf<uint64_t> enc_fsize, enc_foff, enc_zoff;
+  DevBuf<uint8_t> enc_zbuf, enc_out;
+  uint64_t enc_total = 0;               // bytes of the last batch's files (0: none)
+  uint32_t enc_nfiles = 0;
+  std::vector<uint64_t> h_foff;
 
   // timing: ring of per-batch event quintuples (recorded, never waited on in the loop)
   bool timing = true;
@@ -681,8 +694,10 @@ static SceneDev scene_dev(const csg_ctx* c) {
   return s;
 }
 
+// fk: file kinds the batch's images will be encoded to (csg_render_batch):
+// images only a file needs are rendered to internal scratch.
 static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int frames_on_device, const csg_outputs* out,
-                         hipStream_t st) {
+                         hipStream_t st, uint32_t fk = 0) {
   if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "render: no scene uploaded");
   if (!frames || !out || F == 0 || F > c->cfg.max_frames)
     return c->fail(CSG_ERR_INVALID, "render: need 1..%u frames", c->cfg.max_frames);
@@ -773,9 +788,18 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   }
   if (!out->inst_stats) b.stats = nullptr;
   if (!out->label_covered || !out->n_labels) b.covered = nullptr;
+  // images only a file needs go to internal scratch
+  if ((fk & CSG_FILE_RGB_PNG) && !b.rgb) {
+    HIP_TRY(c, c->o_rgb.alloc(F * npx * 3));
+    b.rgb = c->o_rgb.p;
+  }
+  if ((fk & CSG_FILE_DEPTH_CSV) && !b.depth) {
+    HIP_TRY(c, c->o_depth.alloc(F * npx));
+    b.depth = c->o_depth.p;
+  }
   // depth visualisation: needs the depth image (internal scratch when the
   // caller did not ask for depth itself)
-  const bool want_dvis = out->depth_vis || out->depth_range;
+  const bool want_dvis = out->depth_vis || out->depth_range || (fk & CSG_FILE_DEPTH_PNG);
   uint8_t* dvis = nullptr;
   float* drange_out = nullptr;
   if (want_dvis) {
@@ -784,8 +808,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       b.depth = c->o_depth.p;
     }
     HIP_TRY(c, c->drange.alloc((size_t)2 * c->chain_frames));
-    if (out->depth_vis) {
-      if (dev) dvis = out->depth_vis;
+    if (out->depth_vis || (fk & CSG_FILE_DEPTH_PNG)) {
+      if (dev && out->depth_vis) dvis = out->depth_vis;
       else { HIP_TRY(c, c->o_dvis.alloc(F * npx * 3)); dvis = c->o_dvis.p; }
     }
     if (out->depth_range) {
@@ -862,6 +886,9 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     c->last_F = Fc;
   }
   HIP_TRY(c, hipGetLastError());
+  c->last_rgb = b.rgb;
+  c->last_depth = b.depth;
+  c->last_dvis = dvis;
   if (!dev) {
     if (out->rgb) HIP_TRY(c, hipMemcpyAsync(out->rgb, b.rgb, F * npx * 3, hipMemcpyDeviceToHost, st));
     if (out->instance) HIP_TRY(c, hipMemcpyAsync(out->instance, b.inst, F * npx * 4, hipMemcpyDeviceToHost, st));
@@ -872,7 +899,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       HIP_TRY(c, hipMemcpyAsync(out->inst_stats, b.stats, (size_t)F * out->n_labels * 5 * 4, hipMemcpyDeviceToHost, st));
     if (b.covered)
       HIP_TRY(c, hipMemcpyAsync(out->label_covered, b.covered, (size_t)F * out->n_labels * 4, hipMemcpyDeviceToHost, st));
-    if (dvis) HIP_TRY(c, hipMemcpyAsync(out->depth_vis, dvis, F * npx * 3, hipMemcpyDeviceToHost, st));
+    if (out->depth_vis) HIP_TRY(c, hipMemcpyAsync(out->depth_vis, dvis, F * npx * 3, hipMemcpyDeviceToHost, st));
     if (drange_out) HIP_TRY(c, hipMemcpyAsync(out->depth_range, drange_out, (size_t)F * 8, hipMemcpyDeviceToHost, st));
     if (want_kp && out->keypoints_uv)
       HIP_TRY(c, hipMemcpyAsync(out->keypoints_uv, b.kp_uv, (size_t)F * c->n_kp * 8, hipMemcpyDeviceToHost, st));
@@ -887,6 +914,7 @@ int csg_render_batch_async(csg_ctx* c, const csg_frame* frames, uint32_t n_frame
   if (!c) return CSG_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+  if (out && out->file_kinds) return c->fail(CSG_ERR_INVALID, "render: file outputs need csg_render_batch");
   return enqueue_batch(c, frames, n_frames, frames_on_device, out, st);
 }
 
@@ -898,19 +926,94 @@ int csg_synchronize(csg_ctx* c) {
   return take_flags(c, nullptr);
 }
 
+// Copy the last encoded batch's files to host memory (sizes known).
+static int copy_files(csg_ctx* c, uint8_t* dst, uint64_t cap, uint64_t* offsets) {
+  if (offsets) memcpy(offsets, c->h_foff.data(), sizeof(uint64_t) * (c->enc_nfiles + 1));
+  if (c->enc_total > cap || (!dst && c->enc_total))
+    return c->fail(CSG_ERR_CAPACITY, "files: %llu bytes needed, buffer holds %llu",
+                   (unsigned long long)c->enc_total, (unsigned long long)cap);
+  if (c->enc_total) HIP_TRY(c, hipMemcpyAsync(dst, c->enc_out.p, c->enc_total, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return CSG_OK;
+}
+
+// The files of a rendered batch (csg_outputs.file_kinds), encoded on the GPU
+// from the images still in HBM (csg_encode.hip): sizes first, then one
+// synchronisation to size the buffers, then the bytes, then one D2H copy.
+static int encode_files(csg_ctx* c, const csg_outputs* out, uint32_t F) {
+  const uint32_t fk = out->file_kinds;
+  uint32_t nk = 0, slot_rgb = 0, slot_csv = 0, slot_dpng = 0;
+  if (fk & CSG_FILE_RGB_PNG) slot_rgb = nk++;
+  if (fk & CSG_FILE_DEPTH_CSV) slot_csv = nk++;
+  if (fk & CSG_FILE_DEPTH_PNG) slot_dpng = nk++;
+  const uint32_t W = c->cfg.width, H = c->cfg.height, n_files = F * nk;
+  hipStream_t st = c->stream;
+  const size_t rows = (size_t)F * H;
+  HIP_TRY(c, c->enc_fsize.alloc(n_files));
+  HIP_TRY(c, c->enc_foff.alloc(n_files + 1));
+  HIP_TRY(c, c->enc_zoff.alloc(2 * (size_t)F + 1));
+  if (fk & (CSG_FILE_RGB_PNG | CSG_FILE_DEPTH_PNG)) HIP_TRY(c, c->enc_rowsum.alloc(rows));
+  if (fk & CSG_FILE_RGB_PNG) {
+    HIP_TRY(c, c->enc_rgb.alloc(F));
+    HIP_TRY(c, c->enc_rows_rgb.alloc(rows));
+    launch_png_sizes(c->last_rgb, W, H, F, c->enc_rgb.p, c->enc_rowsum.p, c->enc_rows_rgb.p, c->enc_fsize.p, nk,
+                     slot_rgb, st);
+  }
+  if (fk & CSG_FILE_DEPTH_PNG) {
+    HIP_TRY(c, c->enc_dpng.alloc(F));
+    HIP_TRY(c, c->enc_rows_dpng.alloc(rows));
+    launch_png_sizes(c->last_dvis, W, H, F, c->enc_dpng.p, c->enc_rowsum.p, c->enc_rows_dpng.p, c->enc_fsize.p, nk,
+                     slot_dpng, st);
+  }
+  if (fk & CSG_FILE_DEPTH_CSV) {
+    HIP_TRY(c, c->enc_rows_csv.alloc(rows));
+    launch_csv_sizes(c->last_depth, W, H, F, c->enc_rows_csv.p, c->enc_fsize.p, nk, slot_csv, st);
+  }
+  const EncPng* pa = (fk & CSG_FILE_RGB_PNG) ? c->enc_rgb.p : nullptr;
+  const EncPng* pb = (fk & CSG_FILE_DEPTH_PNG) ? c->enc_dpng.p : nullptr;
+  launch_file_layout(c->enc_fsize.p, n_files, c->enc_foff.p, pa, pb, F, c->enc_zoff.p, st);
+  HIP_TRY(c, hipGetLastError());
+  c->h_foff.resize(n_files + 1);
+  uint64_t ztotal = 0;
+  HIP_TRY(c, hipMemcpyAsync(c->h_foff.data(), c->enc_foff.p, sizeof(uint64_t) * (n_files + 1), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(&ztotal, c->enc_zoff.p + 2 * (size_t)F, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  const uint64_t total = c->h_foff[n_files];
+  HIP_TRY(c, c->enc_out.alloc(total + 4));
+  if (ztotal) {
+    HIP_TRY(c, c->enc_zbuf.alloc(ztotal));
+    HIP_TRY(c, hipMemsetAsync(c->enc_zbuf.p, 0, ztotal, st));
+  }
+  if (pa)
+    launch_png_emit(c->last_rgb, W, H, F, pa, c->enc_rows_rgb.p, c->enc_zbuf.p, c->enc_zoff.p, c->enc_out.p,
+                    c->enc_foff.p, nk, slot_rgb, st);
+  if (pb)
+    launch_png_emit(c->last_dvis, W, H, F, pb, c->enc_rows_dpng.p, c->enc_zbuf.p, c->enc_zoff.p + F, c->enc_out.p,
+                    c->enc_foff.p, nk, slot_dpng, st);
+  if (fk & CSG_FILE_DEPTH_CSV)
+    launch_csv_emit(c->last_depth, W, H, F, c->enc_rows_csv.p, c->enc_out.p, c->enc_foff.p, nk, slot_csv, st);
+  HIP_TRY(c, hipGetLastError());
+  c->enc_total = total;
+  c->enc_nfiles = n_files;
+  return copy_files(c, out->files, out->files_cap, out->file_offsets);
+}
+
 int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out) {
   if (!c) return CSG_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   // an earlier asynchronous batch that overflowed is reported, not lost
   int rc = csg_synchronize(c);
   if (rc) return rc;
+  if (out && (out->file_kinds & ~(CSG_FILE_RGB_PNG | CSG_FILE_DEPTH_CSV | CSG_FILE_DEPTH_PNG)))
+    return c->fail(CSG_ERR_INVALID, "render: unknown file kinds %#x", out->file_kinds);
+  const uint32_t fk = out ? out->file_kinds : 0u;
   for (int attempt = 0; attempt < 6; ++attempt) {
-    rc = csg_render_batch_async(c, frames, n_frames, 0, out, nullptr);
+    rc = enqueue_batch(c, frames, n_frames, 0, out, c->stream, fk);
     if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     uint32_t ov = 0;
     HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
-    if (!ov) return CSG_OK;
+    if (!ov) return fk ? encode_files(c, out, n_frames) : CSG_OK;
     HIP_TRY(c, hipMemset(c->overflow.p, 0, 4));
     if (ov & (kOvBadSet | kOvBadKpSet))   // host frames are validated before launch: cannot happen
       return c->fail(CSG_ERR_DEVICE, "render: unexpected set error flags %u", ov);
@@ -937,6 +1040,27 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
     c->work_frames = 0;
   }
   return c->fail(CSG_ERR_OVERFLOW, "work buffers overflowed after growth");
+}
+
+int csg_copy_files(csg_ctx* c, uint8_t* dst, uint64_t cap, uint64_t* offsets) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!c->enc_nfiles) return c->fail(CSG_ERR_INVALID, "copy_files: no batch with files rendered");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  return copy_files(c, dst, cap, offsets);
+}
+
+int csg_host_alloc(csg_ctx* c, uint64_t bytes, void** out) {
+  if (!c || !out) return CSG_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  *out = nullptr;
+  HIP_TRY(c, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return CSG_OK;
+}
+
+int csg_host_free(csg_ctx* c, void* p) {
+  if (!c) return CSG_ERR_INVALID;
+  if (p) HIP_TRY(c, hipHostFree(p));
+  return CSG_OK;
 }
 
 int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {

@@ -1,0 +1,593 @@
+// csg_encode.hip — the generator's files encoded on the GPU from a rendered
+// batch still in HBM (csg_outputs.file_kinds, include/csg_api.h): the RGB
+// PNG and the JET depth PNG (cv2.imwrite, generate_construction_data.py
+// :1672-1673, :1690-1709) and the depth CSV (np.savetxt "%.6f" :1687-1688).
+// The host then only copies the packed bytes out and writes them.
+//
+// Work is parallel over image rows (one thread per row of one frame):
+//
+//   PNG, per image kind (csg_deflate.h for the formats):
+//     k_png_scan    Sub-filter the row on the fly, run-length tokens -> the
+//                   frame's literal/length histogram (LDS, then one atomic
+//                   per symbol per block), Adler-32 sums of the row
+//     k_png_codes   one workgroup per frame: rank sort of the used symbols,
+//                   length-limited Huffman code, canonical codes, zlib +
+//                   dynamic-block header bits, Adler-32 of the frame
+//     k_png_bits    the row's bit count under those codes
+//     k_png_layout  one workgroup per frame: row bit offsets (block scan),
+//                   stream / file size
+//   CSV:
+//     k_csv_len     the row's text length ("%.6f" per value, spaces, "\n")
+//     k_csv_layout  row byte offsets, file size
+//   k_file_layout   offsets of every file of the batch in the packed output
+//                   (and of every PNG's zlib staging area)
+//   -- the host reads the totals and sizes the buffers --
+//   k_png_emit      each row writes its bits at its offset: interior words
+//                   with plain stores, the two words it may share with its
+//                   neighbours with atomicOr (staging zeroed first)
+//   k_png_ends      zlib + block header, end-of-block code, Adler-32
+//   k_png_pack      one thread per 8-KiB IDAT chunk: copy into the file,
+//                   chunk header, CRC-32 (LDS table); signature + IHDR and
+//                   IEND at the ends
+//   k_csv_emit      each row formats its values in place
+//
+// Bandwidth: every pass streams the images once (6.2 MB per 1080p RGB frame,
+// 8.3 MB per depth frame) and the outputs once; the passes are
+// latency-bound per thread but thousands of rows run at once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "csg_deflate.h"
+#include "csg_encode.h"
+
+namespace csg {
+
+using namespace dfl;
+
+namespace {
+
+constexpr int kRowsPerBlock = 64;   // one wave of rows per workgroup (one frame per workgroup)
+
+// Filtered PNG row stream of an 8-bit RGB image row: filter byte 1 (Sub),
+// then each byte minus the byte one pixel (3 bytes) to the left.
+template <class Sink>
+__device__ __forceinline__ void png_row_bytes(const uint8_t* row, uint32_t W, Sink& sink) {
+  sink.push(1u);
+  const uint32_t n = 3u * W;
+  uint32_t h0 = 0, h1 = 0, h2 = 0;   // raw bytes i-3, i-2, i-1
+  const uintptr_t a = reinterpret_cast<uintptr_t>(row);
+  uint32_t i = 0;
+  // head bytes up to a dword boundary, dwords, tail bytes
+  auto one = [&](uint32_t x) {
+    sink.push((x - h0) & 255u);
+    h0 = h1;
+    h1 = h2;
+    h2 = x;
+  };
+  while (i < n && ((a + i) & 3u)) one(row[i++]);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(row + i);
+  const uint32_t nw = (n - i) >> 2;
+  for (uint32_t k = 0; k < nw; ++k) {
+    const uint32_t v = w[k];
+    one(v & 255u);
+    one((v >> 8) & 255u);
+    one((v >> 16) & 255u);
+    one(v >> 24);
+  }
+  i += nw * 4u;
+  while (i < n) one(row[i++]);
+}
+
+// Adler sums of a byte stream starting from (0, 0), reduced lazily.
+struct AdlerSums {
+  uint64_t a = 0, b = 0;
+  uint32_t pending = 0;
+  __device__ __forceinline__ void add(uint32_t x) {
+    a += x;
+    b += a;
+    if (++pending == 4096u) {
+      a %= kAdlerMod;
+      b %= kAdlerMod;
+      pending = 0;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// PNG pass 1: histogram + Adler sums
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kRowsPerBlock) void k_png_scan(const uint8_t* __restrict__ img, uint32_t W, uint32_t H,
+                                                            EncPng* __restrict__ png, uint2* __restrict__ rowsum) {
+  __shared__ uint32_t hist[kLitCodes];
+  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) hist[s] = 0;
+  __syncthreads();
+  if (r < H) {
+    AdlerSums ad;
+    auto lit = [&](uint32_t b) { atomicAdd(&hist[b], 1u); };
+    auto match = [&](uint32_t len) {
+      uint32_t sym, ne, ex;
+      length_code(len, sym, ne, ex);
+      atomicAdd(&hist[sym], 1u);
+    };
+    struct Sink {
+      RunTokenizer<decltype(lit)&, decltype(match)&> tok;
+      AdlerSums* ad;
+      __device__ void push(uint32_t x) {
+        ad->add(x);
+        tok.push(x);
+      }
+    } sink{{lit, match}, &ad};
+    png_row_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, sink);
+    sink.tok.finish();
+    rowsum[(size_t)f * H + r] = make_uint2((uint32_t)(ad.a % kAdlerMod), (uint32_t)(ad.b % kAdlerMod));
+  }
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock)
+    if (hist[s]) atomicAdd(&png[f].hist[s], hist[s]);
+}
+
+// ---------------------------------------------------------------------------
+// PNG pass 2: codes and header (one workgroup of 256 threads per frame)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_png_codes(EncPng* __restrict__ png, const uint2* __restrict__ rowsum,
+                                                   uint32_t W, uint32_t H) {
+  __shared__ uint32_t freq[kLitCodes];
+  __shared__ uint16_t sorted[kLitCodes];
+  __shared__ uint32_t work[kLitCodes];
+  __shared__ uint8_t len[kLitCodes + 1];      // + the one distance code
+  __shared__ uint32_t code[kLitCodes];
+  __shared__ uint16_t tok[kLitCodes + 1];
+  __shared__ uint32_t m_used;
+  const uint32_t f = blockIdx.x, t = threadIdx.x;
+  EncPng& P = png[f];
+  for (uint32_t s = t; s < (uint32_t)kLitCodes; s += 256) {
+    freq[s] = s == kEob ? 1u : P.hist[s];
+    len[s] = 0;
+  }
+  if (t == 0) m_used = 0;
+  __syncthreads();
+  // rank of each used symbol in ascending (frequency, symbol) order
+  for (uint32_t s = t; s < (uint32_t)kLitCodes; s += 256) {
+    const uint32_t fs = freq[s];
+    if (!fs) continue;
+    uint32_t rank = 0;
+    for (uint32_t q = 0; q < (uint32_t)kLitCodes; ++q) {
+      const uint32_t fq = freq[q];
+      rank += (fq && (fq < fs || (fq == fs && q < s))) ? 1u : 0u;
+    }
+    sorted[rank] = (uint16_t)s;
+    atomicAdd(&m_used, 1u);
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int m = (int)m_used;   // >= 2: the filter byte of row 0 and the end-of-block code
+    huff_lengths(freq, sorted, m, kMaxBits, len, work);
+    canonical_codes(len, kLitCodes, code);
+    int hlit = kLitCodes;
+    while (hlit > 257 && len[hlit - 1] == 0) --hlit;
+    len[hlit] = 1;               // one distance code (distance 1), length 1
+    const int ntok = cl_tokens(len, hlit + 1, tok);
+    uint32_t clf[kClCodes] = {0};
+    for (int k = 0; k < ntok; ++k) ++clf[tok[k] & 31u];
+    uint16_t cls[kClCodes];
+    int cm = 0;
+    for (uint32_t s = 0; s < (uint32_t)kClCodes; ++s) {
+      if (!clf[s]) continue;
+      int k = cm++;   // insertion into ascending (frequency, symbol) order
+      while (k > 0 && clf[cls[k - 1]] > clf[s]) {
+        cls[k] = cls[k - 1];
+        --k;
+      }
+      cls[k] = (uint16_t)s;
+    }
+    uint8_t cll[kClCodes] = {0};
+    uint32_t clw[kClCodes];
+    huff_lengths(clf, cls, cm, kMaxClBits, cll, clw);
+    if (cm == 1) cll[cls[0] == 0 ? 1 : 0] = 1;   // the code-length code must be complete
+    uint32_t clc[kClCodes];
+    canonical_codes(cll, kClCodes, clc);
+    int hclen = kClCodes;
+    while (hclen > 4 && cll[cl_order(hclen - 1)] == 0) --hclen;
+    for (uint32_t k = 0; k < kMaxHeaderWords; ++k) P.hdr[k] = 0;
+    BitBuf bb{P.hdr, 0};
+    bb.put(0x78u, 8);            // zlib: deflate, 32 KiB window
+    bb.put(0x01u, 8);            // FCHECK (0x7801 % 31 == 0), no dictionary
+    bb.put(1u, 1);               // BFINAL
+    bb.put(2u, 2);               // BTYPE = dynamic Huffman
+    bb.put((uint32_t)(hlit - 257), 5);
+    bb.put(0u, 5);               // HDIST - 1
+    bb.put((uint32_t)(hclen - 4), 4);
+    for (int k = 0; k < hclen; ++k) bb.put(cll[cl_order(k)], 3);
+    for (int k = 0; k < ntok; ++k) {
+      const uint32_t sym = tok[k] & 31u, ex = (uint32_t)tok[k] >> 8;
+      bb.put(clc[sym] & 0xFFFFu, clc[sym] >> 16);
+      bb.put(ex, cl_extra_bits(sym));
+    }
+    P.hdr_bits = bb.nbits;
+    for (uint32_t s = 0; s < (uint32_t)kLitCodes; ++s) P.code[s] = code[s];
+    // Adler-32 of the whole filtered stream: rows in order from (1, 0)
+    uint32_t a = 1, b = 0;
+    const uint64_t rl = 3ull * W + 1ull;
+    for (uint32_t r = 0; r < H; ++r) {
+      const uint2 v = rowsum[(size_t)f * H + r];
+      adler_cat(a, b, v.x, v.y, rl);
+    }
+    P.adler = (b << 16) | a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PNG pass 3: bits per row
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kRowsPerBlock) void k_png_bits(const uint8_t* __restrict__ img, uint32_t W, uint32_t H,
+                                                            const EncPng* __restrict__ png, uint32_t* __restrict__ rowbits) {
+  __shared__ uint8_t clen[kLitCodes];
+  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) clen[s] = (uint8_t)(png[f].code[s] >> 16);
+  __syncthreads();
+  if (r >= H) return;
+  uint32_t bits = 0;
+  auto lit = [&](uint32_t b) { bits += clen[b]; };
+  auto match = [&](uint32_t len) {
+    uint32_t sym, ne, ex;
+    length_code(len, sym, ne, ex);
+    bits += clen[sym] + ne + 1u;   // + the 1-bit distance code
+  };
+  struct Sink {
+    RunTokenizer<decltype(lit)&, decltype(match)&> tok;
+    __device__ void push(uint32_t x) { tok.push(x); }
+  } sink{{lit, match}};
+  png_row_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, sink);
+  sink.tok.finish();
+  rowbits[(size_t)f * H + r] = bits;
+}
+
+// exclusive scan of n values (in place) over a 256-thread block; returns the total
+__device__ uint32_t block_scan_inplace(uint32_t* v, uint32_t n, uint32_t* sh) {
+  const uint32_t t = threadIdx.x, per = (n + 255u) / 256u, lo = t * per, hi = min(n, lo + per);
+  uint32_t s = 0;
+  for (uint32_t i = lo; i < hi; ++i) s += v[i];
+  sh[t] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256u; o <<= 1) {
+    const uint32_t x = t >= o ? sh[t - o] : 0u;
+    __syncthreads();
+    sh[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = sh[t] - s;
+  const uint32_t total = sh[255];
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+  __syncthreads();
+  return total;
+}
+
+// ---------------------------------------------------------------------------
+// PNG pass 4: row offsets, sizes
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_png_layout(EncPng* __restrict__ png, uint32_t* __restrict__ rowbits, uint32_t H,
+                                                    uint64_t* __restrict__ fsize, uint32_t nk, uint32_t kslot) {
+  __shared__ uint32_t sh[256];
+  const uint32_t f = blockIdx.x;
+  EncPng& P = png[f];
+  const uint32_t total = block_scan_inplace(rowbits + (size_t)f * H, H, sh);
+  if (threadIdx.x == 0) {
+    const uint32_t eob_len = P.code[kEob] >> 16;
+    P.eob_pos = P.hdr_bits + total;
+    const uint32_t zbits = P.eob_pos + eob_len;
+    P.zbytes = (zbits + 7u) / 8u + 4u;
+    const uint32_t nch = (P.zbytes + kIdatBytes - 1u) / kIdatBytes;
+    fsize[(size_t)f * nk + kslot] = 8ull + 25ull + 12ull * nch + P.zbytes + 12ull;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CSV passes
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kRowsPerBlock) void k_csv_len(const float* __restrict__ depth, uint32_t W, uint32_t H,
+                                                           uint32_t* __restrict__ rowlen) {
+  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  if (r >= H) return;
+  const float* row = depth + ((size_t)f * H + r) * W;
+  uint32_t n = W;   // W - 1 spaces and the newline
+  char tmp[kMaxF6Chars];
+  for (uint32_t x = 0; x < W; ++x) n += (uint32_t)fmt6f(row[x], tmp);
+  rowlen[(size_t)f * H + r] = n;
+}
+
+__global__ __launch_bounds__(256) void k_csv_layout(uint32_t* __restrict__ rowlen, uint32_t H, uint64_t* __restrict__ fsize,
+                                                    uint32_t nk, uint32_t kslot) {
+  __shared__ uint32_t sh[256];
+  const uint32_t f = blockIdx.x;
+  const uint32_t total = block_scan_inplace(rowlen + (size_t)f * H, H, sh);
+  if (threadIdx.x == 0) fsize[(size_t)f * nk + kslot] = total;
+}
+
+// Offsets of the batch's files in the packed output (foff[n_files + 1]) and
+// of each PNG frame's zlib staging area (zoff: kind a frames, then kind b
+// frames, then the total; 256-B aligned).  A few hundred entries: one thread.
+__global__ void k_file_layout(const uint64_t* __restrict__ fsize, uint32_t n_files, uint64_t* __restrict__ foff,
+                              const EncPng* __restrict__ png_a, const EncPng* __restrict__ png_b, uint32_t F,
+                              uint64_t* __restrict__ zoff) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t run = 0;
+  for (uint32_t k = 0; k < n_files; ++k) {
+    foff[k] = run;
+    run += fsize[k];
+  }
+  foff[n_files] = run;
+  uint64_t z = 0;
+  for (uint32_t k = 0; k < 2u * F; ++k) {
+    zoff[k] = z;
+    const EncPng* p = k < F ? png_a : png_b;
+    if (p) z += ((uint64_t)p[k < F ? k : k - F].zbytes + 255u) & ~255ull;
+  }
+  zoff[2u * F] = z;
+}
+
+// ---------------------------------------------------------------------------
+// PNG emission
+// ---------------------------------------------------------------------------
+// LSB-first bits into zeroed staging words from bit `pos`: the first word
+// (possibly shared with the previous row) and the last (possibly shared with
+// the next) with atomicOr, words in between with plain stores.
+struct WordBits {
+  uint32_t* w;
+  uint64_t acc;
+  uint32_t n, wi;
+  bool first;
+  __device__ void init(uint32_t* words, uint32_t pos) {
+    w = words;
+    wi = pos >> 5;
+    n = pos & 31u;
+    acc = 0;
+    first = true;
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t len) {
+    acc |= (uint64_t)v << n;
+    n += len;
+    if (n >= 32u) {
+      const uint32_t word = (uint32_t)acc;
+      if (first) atomicOr(&w[wi], word);
+      else w[wi] = word;
+      first = false;
+      ++wi;
+      acc >>= 32;
+      n -= 32u;
+    }
+  }
+  __device__ void finish() {
+    if (n) atomicOr(&w[wi], (uint32_t)acc);
+  }
+};
+
+__global__ __launch_bounds__(kRowsPerBlock) void k_png_emit(const uint8_t* __restrict__ img, uint32_t W, uint32_t H,
+                                                            const EncPng* __restrict__ png,
+                                                            const uint32_t* __restrict__ rowoff, uint8_t* zbuf,
+                                                            const uint64_t* __restrict__ zbase) {
+  __shared__ uint32_t code[kLitCodes];
+  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) code[s] = png[f].code[s];
+  __syncthreads();
+  if (r >= H) return;
+  uint32_t* words = reinterpret_cast<uint32_t*>(zbuf + zbase[f]);
+  WordBits wb;
+  wb.init(words, png[f].hdr_bits + rowoff[(size_t)f * H + r]);
+  auto lit = [&](uint32_t b) { wb.put(code[b] & 0xFFFFu, code[b] >> 16); };
+  auto match = [&](uint32_t len) {
+    uint32_t sym, ne, ex;
+    length_code(len, sym, ne, ex);
+    wb.put(code[sym] & 0xFFFFu, code[sym] >> 16);
+    wb.put(ex, ne);
+    wb.put(0u, 1u);   // distance code 0 (distance 1), code "0"
+  };
+  struct Sink {
+    RunTokenizer<decltype(lit)&, decltype(match)&> tok;
+    __device__ void push(uint32_t x) { tok.push(x); }
+  } sink{{lit, match}};
+  png_row_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, sink);
+  sink.tok.finish();
+  wb.finish();
+}
+
+// header words, end-of-block code, Adler-32 (big-endian) after the padding
+__global__ __launch_bounds__(64) void k_png_ends(const EncPng* __restrict__ png, uint8_t* zbuf,
+                                                 const uint64_t* __restrict__ zbase) {
+  const uint32_t f = blockIdx.x;
+  const EncPng& P = png[f];
+  uint32_t* words = reinterpret_cast<uint32_t*>(zbuf + zbase[f]);
+  const uint32_t nh = (P.hdr_bits + 31u) / 32u;
+  for (uint32_t k = threadIdx.x; k < nh; k += 64) atomicOr(&words[k], P.hdr[k]);
+  if (threadIdx.x == 0) {
+    const uint32_t c = P.code[kEob], l = c >> 16, pos = P.eob_pos;
+    const uint64_t v = (uint64_t)(c & 0xFFFFu) << (pos & 31u);
+    atomicOr(&words[pos >> 5], (uint32_t)v);
+    if ((pos & 31u) + l > 32u) atomicOr(&words[(pos >> 5) + 1], (uint32_t)(v >> 32));
+    const uint32_t at = P.zbytes - 4u;   // byte index of the Adler-32
+    const uint32_t be = __builtin_bswap32(P.adler);
+    const uint64_t sv = (uint64_t)be << (8u * (at & 3u));
+    atomicOr(&words[at >> 2], (uint32_t)sv);
+    if (at & 3u) atomicOr(&words[(at >> 2) + 1], (uint32_t)(sv >> 32));
+  }
+}
+
+// Bytes to an arbitrary offset: byte stores up to a dword boundary, then
+// whole dwords, the tail again as bytes.
+struct ByteOut {
+  uint8_t* base;
+  uint64_t pos;
+  uint32_t acc, na;
+  __device__ void init(uint8_t* b, uint64_t p) {
+    base = b;
+    pos = p;
+    acc = 0;
+    na = 0;
+  }
+  __device__ __forceinline__ void put(uint32_t c) {
+    if (na == 0 && (pos & 3u)) {
+      base[pos++] = (uint8_t)c;
+      return;
+    }
+    acc |= (c & 255u) << (8u * na);
+    ++pos;
+    if (++na == 4u) {
+      *reinterpret_cast<uint32_t*>(base + pos - 4u) = acc;
+      acc = 0;
+      na = 0;
+    }
+  }
+  __device__ void be32(uint32_t v) {
+    put(v >> 24);
+    put((v >> 16) & 255u);
+    put((v >> 8) & 255u);
+    put(v & 255u);
+  }
+  __device__ void finish() {
+    for (uint32_t k = 0; k < na; ++k) base[pos - na + k] = (uint8_t)(acc >> (8u * k));
+    na = 0;
+    acc = 0;
+  }
+};
+
+struct Crc {
+  const uint32_t* T;
+  uint32_t c;
+  __device__ __forceinline__ void add(uint32_t b) { c = T[(c ^ b) & 255u] ^ (c >> 8); }
+};
+
+__global__ __launch_bounds__(64) void k_png_pack(const EncPng* __restrict__ png, const uint8_t* __restrict__ zbuf,
+                                                 const uint64_t* __restrict__ zbase, uint8_t* out,
+                                                 const uint64_t* __restrict__ foff, uint32_t W, uint32_t H, uint32_t nk,
+                                                 uint32_t kslot) {
+  __shared__ uint32_t T[256];
+  for (uint32_t k = threadIdx.x; k < 256u; k += 64) T[k] = crc_entry(k);
+  __syncthreads();
+  const uint32_t f = blockIdx.y, ch = blockIdx.x * 64u + threadIdx.x;
+  const EncPng& P = png[f];
+  const uint32_t zb = P.zbytes, nch = (zb + kIdatBytes - 1u) / kIdatBytes;
+  if (ch >= nch) return;
+  uint8_t* file = out + foff[(size_t)f * nk + kslot];
+  const uint32_t n = min(kIdatBytes, zb - ch * kIdatBytes);
+  ByteOut o;
+  if (ch == 0) {   // signature + IHDR
+    o.init(file, 0);
+    const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    for (int k = 0; k < 8; ++k) o.put(sig[k]);
+    o.be32(13u);
+    Crc c{T, 0xFFFFFFFFu};
+    const uint8_t ihdr[17] = {'I', 'H', 'D', 'R', (uint8_t)(W >> 24), (uint8_t)(W >> 16), (uint8_t)(W >> 8), (uint8_t)W,
+                              (uint8_t)(H >> 24), (uint8_t)(H >> 16), (uint8_t)(H >> 8), (uint8_t)H, 8, 2, 0, 0, 0};
+    for (int k = 0; k < 17; ++k) {
+      o.put(ihdr[k]);
+      c.add(ihdr[k]);
+    }
+    o.be32(c.c ^ 0xFFFFFFFFu);
+    o.finish();
+  }
+  const uint64_t at = 33ull + (uint64_t)ch * (kIdatBytes + 12u);
+  o.init(file, at);
+  o.be32(n);
+  Crc c{T, 0xFFFFFFFFu};
+  const uint8_t idat[4] = {'I', 'D', 'A', 'T'};
+  for (int k = 0; k < 4; ++k) {
+    o.put(idat[k]);
+    c.add(idat[k]);
+  }
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(zbuf + zbase[f] + (size_t)ch * kIdatBytes);
+  const uint32_t nw = n >> 2;
+  for (uint32_t k = 0; k < nw; ++k) {
+    const uint32_t v = src[k];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t b = (v >> (8 * s)) & 255u;
+      o.put(b);
+      c.add(b);
+    }
+  }
+  if (n & 3u) {
+    const uint32_t v = src[nw];
+    for (uint32_t s = 0; s < (n & 3u); ++s) {
+      const uint32_t b = (v >> (8u * s)) & 255u;
+      o.put(b);
+      c.add(b);
+    }
+  }
+  o.be32(c.c ^ 0xFFFFFFFFu);
+  if (ch == nch - 1u) {   // IEND
+    o.be32(0u);
+    const uint8_t iend[8] = {'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+    for (int k = 0; k < 8; ++k) o.put(iend[k]);
+  }
+  o.finish();
+}
+
+__global__ __launch_bounds__(kRowsPerBlock) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
+                                                            const uint32_t* __restrict__ rowoff, uint8_t* out,
+                                                            const uint64_t* __restrict__ foff, uint32_t nk,
+                                                            uint32_t kslot) {
+  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  if (r >= H) return;
+  const float* row = depth + ((size_t)f * H + r) * W;
+  ByteOut o;
+  o.init(out, foff[(size_t)f * nk + kslot] + rowoff[(size_t)f * H + r]);
+  char tmp[kMaxF6Chars];
+  for (uint32_t x = 0; x < W; ++x) {
+    const int n = fmt6f(row[x], tmp);
+    for (int k = 0; k < n; ++k) o.put((uint8_t)tmp[k]);
+    o.put(x + 1u < W ? ' ' : '\n');
+  }
+  o.finish();
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launchers (csg_encode.h)
+// ---------------------------------------------------------------------------
+void launch_png_sizes(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, EncPng* png, uint2* rowsum,
+                      uint32_t* rowbits, uint64_t* fsize, uint32_t nk, uint32_t kslot, hipStream_t st) {
+  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
+  (void)hipMemsetAsync(png, 0, sizeof(EncPng) * F, st);
+  hipLaunchKernelGGL(k_png_scan, rows, dim3(kRowsPerBlock), 0, st, img, W, H, png, rowsum);
+  hipLaunchKernelGGL(k_png_codes, dim3(F), dim3(256), 0, st, png, rowsum, W, H);
+  hipLaunchKernelGGL(k_png_bits, rows, dim3(kRowsPerBlock), 0, st, img, W, H, png, rowbits);
+  hipLaunchKernelGGL(k_png_layout, dim3(F), dim3(256), 0, st, png, rowbits, H, fsize, nk, kslot);
+}
+
+void launch_csv_sizes(const float* depth, uint32_t W, uint32_t H, uint32_t F, uint32_t* rowlen, uint64_t* fsize,
+                      uint32_t nk, uint32_t kslot, hipStream_t st) {
+  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
+  hipLaunchKernelGGL(k_csv_len, rows, dim3(kRowsPerBlock), 0, st, depth, W, H, rowlen);
+  hipLaunchKernelGGL(k_csv_layout, dim3(F), dim3(256), 0, st, rowlen, H, fsize, nk, kslot);
+}
+
+void launch_file_layout(const uint64_t* fsize, uint32_t n_files, uint64_t* foff, const EncPng* png_a,
+                        const EncPng* png_b, uint32_t F, uint64_t* zoff, hipStream_t st) {
+  hipLaunchKernelGGL(k_file_layout, dim3(1), dim3(64), 0, st, fsize, n_files, foff, png_a, png_b, F, zoff);
+}
+
+void launch_png_emit(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, const EncPng* png, const uint32_t* rowoff,
+                     uint8_t* zbuf, const uint64_t* zbase, uint8_t* out, const uint64_t* foff, uint32_t nk,
+                     uint32_t kslot, hipStream_t st) {
+  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
+  hipLaunchKernelGGL(k_png_emit, rows, dim3(kRowsPerBlock), 0, st, img, W, H, png, rowoff, zbuf, zbase);
+  hipLaunchKernelGGL(k_png_ends, dim3(F), dim3(64), 0, st, png, zbuf, zbase);
+  // chunks per frame: at most the worst-case stream size / 8 KiB
+  const uint64_t max_z = (uint64_t)H * (3ull * W + 1ull) * 2ull + 65536ull;
+  const uint32_t max_ch = (uint32_t)((max_z + kIdatBytes - 1) / kIdatBytes);
+  hipLaunchKernelGGL(k_png_pack, dim3((max_ch + 63) / 64, F), dim3(64), 0, st, png, zbuf, zbase, out, foff, W, H, nk,
+                     kslot);
+}
+
+void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,
+                     const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
+  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
+  hipLaunchKernelGGL(k_csv_emit, rows, dim3(kRowsPerBlock), 0, st, depth, W, H, rowoff, out, foff, nk, kslot);
+}
+
+}  // namespace csg

@@ -101,6 +101,7 @@ class Renderer:
         self.n_labels = max(self.packed.n_labels, 1)
         assert self.n_labels == scene_labels(scene)
         self.n_kp = 0
+        self._pinned: List[C.c_void_p] = []
         self._upload()
 
     # -- lifecycle ------------------------------------------------------------
@@ -111,6 +112,9 @@ class Renderer:
 
     def close(self) -> None:
         if getattr(self, "ctx", None):
+            for p in getattr(self, "_pinned", []):
+                self.lib.csg_host_free(self.ctx, p)
+            self._pinned = []
             self.lib.csg_destroy(self.ctx)
             self.ctx = None
 
@@ -222,6 +226,71 @@ class Renderer:
                         "render_batch")
         return out
 
+    # -- files encoded on the GPU --------------------------------------------------
+    def host_buffer(self, nbytes: int) -> np.ndarray:
+        """A page-locked uint8 host array of ``nbytes`` (csg_host_alloc), freed
+        with the renderer; D2H copies into it run at full PCIe rate."""
+        p = C.c_void_p()
+        self._check(self.lib.csg_host_alloc(self.ctx, int(nbytes), C.byref(p)), "host_alloc")
+        buf = (C.c_uint8 * int(nbytes)).from_address(p.value)
+        arr = np.frombuffer(buf, np.uint8)
+        self._pinned.append(p)
+        return arr
+
+    def render_files(self, frames: np.ndarray, kinds: Sequence[str], files: np.ndarray,
+                     want: Iterable[str] = (), out: Optional[Dict[str, np.ndarray]] = None):
+        """Render a batch (at most ``max_frames``) and encode ``kinds`` (of
+        ``_lib.FILE_KINDS``: "rgb_png", "depth_csv", "depth_png") on the GPU
+        into ``files`` (uint8 host array, pinned from :meth:`host_buffer` for
+        speed), growing nothing: returns (outputs dict as :meth:`render`,
+        offsets) with file j = frame * len(kinds) + k (kinds in bit order) at
+        ``files[offsets[j]:offsets[j + 1]]``; ``None`` offsets' last entry
+        says how many bytes were needed when ``files`` was too small (the
+        files stay on the device: :meth:`copy_files`)."""
+        frames = np.ascontiguousarray(frames, FRAME_DTYPE)
+        n = frames.shape[0]
+        if n > self.max_frames:
+            raise CsgError(f"render_files: {n} frames > max_frames {self.max_frames}")
+        mask = 0
+        for k in kinds:
+            if k not in _lib.FILE_KINDS:
+                raise CsgError(f"unknown file kind {k!r}; choose from {tuple(_lib.FILE_KINDS)}")
+            mask |= _lib.FILE_KINDS[k]
+        spec = self.output_spec(n, want)
+        if out is None:
+            out = {k: np.empty(shape, dt) for k, (shape, dt) in spec.items()}
+        else:
+            for k, (shape, dt) in spec.items():
+                a = out.get(k)
+                if a is None or a.shape != shape or a.dtype != dt or not a.flags.c_contiguous:
+                    raise CsgError(f"render_files: out[{k!r}] must be a C-contiguous {np.dtype(dt)} array of shape {shape}")
+            out = {k: out[k] for k in spec}
+        nk = bin(mask).count("1")
+        offsets = np.zeros(n * nk + 1, np.uint64)
+        if files.dtype != np.uint8 or not files.flags.c_contiguous:
+            raise CsgError("render_files: files must be a C-contiguous uint8 array")
+        oo = _lib.Outputs()
+        for key in ("rgb", "instance", "depth", "keypoints_uv", "keypoints_vis", "inst_stats", "normals", "points",
+                    "depth_vis", "depth_range", "label_covered"):
+            arr = out.get(key)
+            if arr is not None:
+                setattr(oo, key, arr.ctypes.data)
+        oo.n_labels, oo.on_device = self.n_labels, 0
+        oo.file_kinds, oo.files, oo.files_cap, oo.file_offsets = mask, files.ctypes.data, files.nbytes, offsets.ctypes.data
+        rc = self.lib.csg_render_batch(self.ctx, frames.ctypes.data, n, C.byref(oo))
+        if rc == _lib.ERR_CAPACITY:
+            return out, None, int(offsets[-1])
+        self._check(rc, "render_batch (files)")
+        return out, offsets, int(offsets[-1])
+
+    def copy_files(self, files: np.ndarray, n_files: int) -> np.ndarray:
+        """The last :meth:`render_files` batch's files again (after the
+        buffer was too small): returns the offsets."""
+        offsets = np.zeros(n_files + 1, np.uint64)
+        self._check(self.lib.csg_copy_files(self.ctx, files.ctypes.data, files.nbytes, offsets.ctypes.data),
+                    "copy_files")
+        return offsets
+
     def render_into(self, frames_ptr: int, n: int, frames_on_device: bool, rgb: int = 0, instance: int = 0,
                     depth: int = 0, kp_uv: int = 0, kp_vis: int = 0, stats: int = 0, stream: int = 0,
                     normals: int = 0, points: int = 0, depth_vis: int = 0, depth_range: int = 0,
@@ -229,7 +298,7 @@ class Renderer:
         """Enqueue a batch writing device buffers (raw pointers, e.g. torch ``data_ptr()``)."""
         o = _lib.Outputs(rgb or None, instance or None, depth or None, kp_uv or None, kp_vis or None,
                          stats or None, self.n_labels, 1, normals or None, points or None, depth_vis or None,
-                         depth_range or None, covered or None)
+                         depth_range or None, covered or None, 0, 0, None, 0, None)
         self._check(self.lib.csg_render_batch_async(self.ctx, frames_ptr, n, int(frames_on_device), C.byref(o),
                                                     stream or None), "render_batch_async")
 

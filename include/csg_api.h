@@ -26,6 +26,11 @@
  *                                                                     :1681, :1475/:1909
  *   csg_project_keypoints ..... 3D->2D projection with the frame's
  *                               intrinsics (pinhole of :646-649)
+ *   csg_outputs.file_kinds .... the frame's files encoded on the GPU:
+ *                               cv2.imwrite of the RGB and JET depth
+ *                               images, np.savetxt of the depth  :1672-1673,
+ *                                                                :1687-1709
+ *   csg_copy_files / csg_host_alloc / csg_host_free (pinned buffers for them)
  *   csg_last_error / csg_destroy
  *
  * Threading: one context per device per process; a context is not
@@ -40,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 7
+#define CSG_ABI_VERSION 8
 
 typedef enum {
   CSG_OK = 0,
@@ -48,7 +53,9 @@ typedef enum {
   CSG_ERR_DEVICE = -2,       /* HIP runtime error */
   CSG_ERR_OOM = -3,          /* device allocation failed */
   CSG_ERR_OVERFLOW = -4,     /* a per-frame work buffer overflowed; raise caps */
-  CSG_ERR_LIMIT = -5         /* scene exceeds a fixed limit (instances, tris/mesh) */
+  CSG_ERR_LIMIT = -5,        /* scene exceeds a fixed limit (instances, tris/mesh) */
+  CSG_ERR_CAPACITY = -6      /* csg_outputs.files too small: file_offsets[n_files] holds the
+                                bytes needed; csg_copy_files fetches them without rendering again */
 } csg_status;
 
 typedef struct csg_ctx csg_ctx;
@@ -127,7 +134,28 @@ typedef struct {
                                 passes the alpha test (no depth test).  Bit 31 set = unknown
                                 (a 32x32 tile held more than 32 labels).  occlusionRatio =
                                 1 - pixels / covered (bounding_box_3d, GDP:1780-1790) */
+  /* Files encoded on the GPU (csg_render_batch only, not the async form).
+   * file_kinds: bit set of CSG_FILE_*; per frame one file per kind, in bit
+   * order: file j = frame * n_kinds + k.  The packed bytes of all files go to
+   * `files` (host memory, files_cap bytes; pinned memory from csg_host_alloc
+   * copies at full PCIe rate), file j at [file_offsets[j], file_offsets[j + 1])
+   * (file_offsets: n_frames * n_kinds + 1 entries).  The images a kind needs
+   * are rendered to internal scratch when the caller did not ask for them. */
+  uint32_t file_kinds;
+  uint32_t pad_files;
+  uint8_t* files;
+  uint64_t files_cap;
+  uint64_t* file_offsets;
 } csg_outputs;
+
+/* csg_outputs.file_kinds */
+#define CSG_FILE_RGB_PNG 1u        /* 8-bit RGB PNG of the frame (cv2.imwrite, GDP:1672-1673): filter Sub,
+                                      one dynamic-Huffman deflate block of literals and distance-1 matches,
+                                      8 KiB IDAT chunks */
+#define CSG_FILE_DEPTH_CSV 2u      /* np.savetxt(depth, fmt="%.6f", delimiter=" ") text (GDP:1687-1688),
+                                      byte-identical */
+#define CSG_FILE_DEPTH_PNG 4u      /* the JET depth visualisation (csg_outputs.depth_vis) as a PNG
+                                      (GDP:1690-1709) */
 
 typedef struct {
   uint64_t records;          /* raster triangles emitted (all frames of the last launch chain) */
@@ -206,6 +234,14 @@ int csg_timing_read(csg_ctx* ctx, csg_timing* out);
  * out [n_instances][6] = xmin, ymin, zmin, xmax, ymax, zmax (host buffer);
  * the GPU side of the bounding_box_3d annotator (GDP:1780-1790). */
 int csg_instance_bounds(csg_ctx* ctx, uint32_t set_id, float* out);
+
+/* The files of the last csg_render_batch that asked for files, again
+ * (after CSG_ERR_CAPACITY): dst host memory of cap bytes; offsets as
+ * csg_outputs.file_offsets (may be NULL). */
+int csg_copy_files(csg_ctx* ctx, uint8_t* dst, uint64_t cap, uint64_t* offsets);
+/* Page-locked host memory for csg_outputs.files and the other host outputs. */
+int csg_host_alloc(csg_ctx* ctx, uint64_t bytes, void** out);
+int csg_host_free(csg_ctx* ctx, void* p);
 
 /* Stand-alone 3D->2D projection (host buffers): uv [n][2], vis [n] without a
  * depth test (1 = in front and inside the image, 0 otherwise). */

@@ -1,0 +1,92 @@
+"""Files encoded on the GPU (csg_outputs.file_kinds, csg_encode.hip) against
+independent decoders and writers:
+
+* RGB PNG and JET depth PNG (cv2.imwrite, generate_construction_data.py
+  :1672-1673, :1690-1709): zlib (Python's, an independent inflater) must
+  decode them to exactly the rendered RGB / depth_vis images, with every
+  chunk CRC and the Adler-32 checked (tests/pngutil.py);
+* depth CSV (np.savetxt(depth, fmt="%.6f", delimiter=" "), :1687-1688):
+  byte-identical to np.savetxt of the rendered depth;
+
+on the headline C3 workload at 1920x1080 (frames of the bench's schedule),
+a ragged size (partial rows of every kind: 203x117) and a frame that sees
+nothing (flat PNGs, "inf" text); plus the too-small-buffer path
+(CSG_ERR_CAPACITY, then csg_copy_files).
+"""
+import io
+
+import numpy as np
+import pytest
+
+from pngutil import decode_png
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("rgb_png", "depth_csv", "depth_png")
+
+
+def _render(wl, frames, W=None, H=None, views=None, projs=None, cap=None):
+    from constructionsceneposeestimation_amd.renderer import Renderer, make_frames
+    W, H = W or wl.width, H or wl.height
+    epochs = sorted({f // 10 for f in frames})
+    if views is None:
+        views, projs = wl.frame_params(frames)
+    with Renderer(wl.scene, W, H, max_frames=len(frames)) as r:
+        for k, e in enumerate(epochs):
+            r.set_instance_transforms(k, wl.epoch(e).models)
+        fr = make_frames(views, projs, [epochs.index(f // 10) for f in frames], frames)
+        files = r.host_buffer(cap or len(frames) * H * W * 16 + (1 << 20))
+        out, offsets, need = r.render_files(fr, KINDS, files, want=("rgb", "depth", "depth_vis"))
+        if cap is not None:
+            assert offsets is None and need > cap
+            big = r.host_buffer(need)
+            offsets = r.copy_files(big, len(frames) * len(KINDS))
+            files = big
+        assert offsets is not None and int(offsets[-1]) == need
+        blobs = [bytes(files[int(offsets[j]):int(offsets[j + 1])]) for j in range(len(offsets) - 1)]
+    return out, blobs
+
+
+def _check(out, blobs, n):
+    for f in range(n):
+        png, csv, dpng = blobs[3 * f:3 * f + 3]
+        assert np.array_equal(decode_png(png), out["rgb"][f]), f"frame {f}: rgb png"
+        assert np.array_equal(decode_png(dpng), out["depth_vis"][f]), f"frame {f}: depth png"
+        ref = io.BytesIO()
+        np.savetxt(ref, out["depth"][f], fmt="%.6f", delimiter=" ")
+        assert csv == ref.getvalue(), f"frame {f}: depth csv"
+
+
+def test_files_c3_1080p():
+    from constructionsceneposeestimation_amd.workload import Workload
+    wl = Workload("C3", seed=0)
+    frames = [1200, 1517, 2323]
+    out, blobs = _render(wl, frames)
+    _check(out, blobs, len(frames))
+    # compressed: the RGB PNG well below the raw image, the CSV at its text size
+    assert len(blobs[0]) < 0.6 * 1920 * 1080 * 3
+
+
+def test_files_ragged_and_empty_frame():
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd.workload import Workload
+    wl = Workload("C3", seed=0)
+    W, H = 203, 117
+    intr = cm.Intrinsics(W, H)
+    views, projs = [], []
+    for cam, aim in (([-3.0, -3.0, 1.6], [0.0, 0.0, 1.6]), ([0.0, 0.0, 200.0], [0.0, 0.0, 400.0]),
+                     ([6.0, 0.0, 2.5], [0.0, 0.0, 2.5])):
+        V, P, _ = cm.frame_matrices(cam, cm.look_at_world_quat(cam, aim), intr)
+        views.append(V)
+        projs.append(P)
+    frames = [0, 1, 2]
+    out, blobs = _render(wl, frames, W, H, np.stack(views), np.stack(projs))
+    assert np.isinf(out["depth"][1]).all()   # the sky frame: flat images, "inf" text
+    _check(out, blobs, len(frames))
+
+
+def test_files_buffer_too_small_then_copy():
+    from constructionsceneposeestimation_amd.workload import Workload
+    wl = Workload("C3", seed=0)
+    out, blobs = _render(wl, [1200, 1201], 480, 272, cap=4096)
+    _check(out, blobs, 2)

@@ -11,11 +11,11 @@ src=constructionsceneposeestimation_amd/csrc
 tmp=$(mktemp -d)
 mkdir -p $tmp/pkg/csrc $tmp/include
 cp include/csg_api.h $tmp/include/
-cp $src/csg_api.cpp $src/csg_kernels.hip $src/csg_kernels.h $tmp/pkg/csrc/
+cp $src/csg_api.cpp $src/csg_kernels.hip $src/csg_kernels.h $src/csg_encode.hip $src/csg_encode.h $src/csg_deflate.h $tmp/pkg/csrc/
 if [ "$rev" != "-" ]; then
   for f in csg_kernels.hip csg_kernels.h; do git show $rev:$src/$f > $tmp/pkg/csrc/$f; done
 fi
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared -ffp-contract=off --offload-arch=gfx950 -Wall "$@" \
-  -o constructionsceneposeestimation_amd/libcsg_$name.so $tmp/pkg/csrc/csg_kernels.hip $tmp/pkg/csrc/csg_api.cpp
+  -o constructionsceneposeestimation_amd/libcsg_$name.so $tmp/pkg/csrc/csg_kernels.hip $tmp/pkg/csrc/csg_encode.hip $tmp/pkg/csrc/csg_api.cpp
 rm -rf $tmp
 echo built constructionsceneposeestimation_amd/libcsg_$name.so
