@@ -24,6 +24,9 @@ IO_LIB = os.path.join(PKG, "libcsgio.so")
 IO_SOURCES = [os.path.join(PKG, "csrc", "csg_io.cpp")]
 IO_DEPS = IO_SOURCES + [os.path.join(ROOT, "include", "csg_io.h")]
 IO_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread"]
+# _csgjson: the label-JSON encoder (CPython extension module)
+JSON_EXT = os.path.join(PKG, "_csgjson.so")
+JSON_SOURCES = [os.path.join(PKG, "csrc", "csg_json.cpp")]
 
 # -ffp-contract=off: the raster spec's float expressions must round exactly as
 # written (bit-exact with the CPU oracle).  HIP keeps fp32 '/' and sqrtf
@@ -67,6 +70,20 @@ def build_io(force: bool = False, verbose: bool = False) -> str:
     return IO_LIB
 
 
+def build_json(force: bool = False, verbose: bool = False) -> str:
+    if force or needs_build(JSON_EXT, JSON_SOURCES):
+        import sysconfig
+        cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+        cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{sysconfig.get_paths()['include']}", "-o",
+               JSON_EXT + ".tmp", *JSON_SOURCES]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(JSON_EXT + ".tmp", JSON_EXT)
+    return JSON_EXT
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_io(force="--force" in sys.argv, verbose=True))
+    print(build_json(force="--force" in sys.argv, verbose=True))

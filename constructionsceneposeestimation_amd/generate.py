@@ -36,6 +36,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
 import numpy as np
@@ -108,43 +109,80 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         os.makedirs(os.path.join(out_dir, d), exist_ok=True)
     if resume:
         frames = [f for f in frames if not os.path.exists(os.path.join(out_dir, "labels", f"label_{f:06d}.json"))]
-    host_depth = bool(outs & {"depth_csv", "depth_npy", "pointcloud"})
+    # Thread writers (the default): the PNGs and the depth CSV are encoded on
+    # the GPU (Renderer.render_files, csg_encode.hip) and the host only writes
+    # bytes; writer processes encode on the host (libcsgio).
+    gpu_files = writer_mode == "thread"
+    kinds = tuple(k for o, k in (("rgb", "rgb_png"), ("depth_csv", "depth_csv"), ("depth_png", "depth_png"))
+                  if o in outs) if gpu_files else ()
+    # host depth: for its own files, and for the quality log's depth counts
+    host_depth = bool(outs & {"depth_npy", "pointcloud", "depth_csv"})
     log = QualityLog(os.path.join(out_dir, "logs"))
-    want = (["rgb", "instance", "keypoints", "stats", "covered"] + (["depth"] if host_depth else [])
-            + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
-            + (["normals"] if "normals" in outs else []))
+    if gpu_files:
+        want = (["keypoints", "stats", "covered"] + (["instance"] if "mask" in outs else [])
+                + (["depth"] if host_depth else []) + (["depth_range"] if "depth_png" in outs else [])
+                + (["points", "rgb"] if "pointcloud" in outs else []) + (["normals"] if "normals" in outs else []))
+    else:
+        want = (["rgb", "instance", "keypoints", "stats", "covered"] + (["depth"] if host_depth else [])
+                + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
+                + (["normals"] if "normals" in outs else []))
     n_writers = writers or default_writers()
     # the writer processes start here, before this process touches the GPU
     pool = WriterPool(output_spec(batch, wl.height, wl.width, wl.n_keypoints(), scene_labels(wl.scene), want),
                       n_writers, n_slots=3, mode=writer_mode)
     r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
+    if kinds:   # pinned buffers for the encoded files: a generous estimate, grown on demand
+        npx = wl.width * wl.height
+        est = {"rgb_png": 2 * npx, "depth_csv": 10 * npx, "depth_png": npx}
+        pool.set_files_buffers(r.host_buffer, batch * sum(est[k] for k in kinds) + (1 << 20))
+    nk = len(kinds)
     intr = wl.intr
     pose_cache = {}
     pending = []
     t_render = 0.0
     t0 = time.time()
+    starts = list(range(0, len(frames), batch))
+
+    def render_batch(b: int):
+        """Batch b into its slot of the writer ring (runs one batch ahead of
+        the label loop, in its own thread: the C-ABI call releases the GIL)."""
+        fb = frames[starts[b]:starts[b] + batch]
+        slot = b % pool.n_slots
+        arrays = pool.arrays(slot)          # (waits until the writers are done with the slot)
+        epochs = sorted({f // 10 for f in fb})
+        set_of = {}
+        for k, e in enumerate(epochs):
+            st = wl.epoch(e)
+            r.set_instance_transforms(k, st.models)
+            r.set_keypoints(k, st.keypoints)
+            if st.dr is not None:
+                r.set_dr_light(k, st.dr.light)
+                r.set_dr_textures(k, st.dr.textures)
+            set_of[e] = k
+        views, projs = wl.frame_params(fb)
+        tr = time.time()
+        fr = make_frames(views, projs, [set_of[f // 10] for f in fb], fb)
+        if kinds:
+            outs_b = {k: v[:len(fb)] for k, v in arrays.items() if k not in ("files", "file_offsets")}
+            out, offsets, need = r.render_files(fr, kinds, arrays["files"], want=want, out=outs_b)
+            if offsets is None:   # the files did not fit: a larger buffer, no re-render
+                offsets = r.copy_files(pool.grow_files(slot, need + need // 4), len(fb) * nk)
+            arrays["file_offsets"] = offsets
+        else:
+            out = r.render(fr, want=want, out={k: v[:len(fb)] for k, v in arrays.items()})
+        return fb, slot, out, time.time() - tr
+
+    ahead = ThreadPoolExecutor(max_workers=1)
     try:
-        for b, s0 in enumerate(range(0, len(frames), batch)):
-            fb = frames[s0:s0 + batch]
-            slot = b % pool.n_slots
-            arrays = pool.arrays(slot)          # (waits until the writers are done with the slot)
-            epochs = sorted({f // 10 for f in fb})
-            set_of = {}
-            for k, e in enumerate(epochs):
-                st = wl.epoch(e)
-                r.set_instance_transforms(k, st.models)
-                r.set_keypoints(k, st.keypoints)
-                if st.dr is not None:
-                    r.set_dr_light(k, st.dr.light)
-                    r.set_dr_textures(k, st.dr.textures)
-                set_of[e] = k
+        nxt = ahead.submit(render_batch, 0) if starts else None
+        for b in range(len(starts)):
+            fb, slot, out, dt = nxt.result()
+            t_render += dt
+            if b + 1 < len(starts):
+                nxt = ahead.submit(render_batch, b + 1)
+            for e in sorted({f // 10 for f in fb}):
                 if e not in pose_cache:
-                    pose_cache[e] = object_poses(wl.scene, st.object_frames)
-            views, projs = wl.frame_params(fb)
-            tr = time.time()
-            out = r.render(make_frames(views, projs, [set_of[f // 10] for f in fb], fb), want=want,
-                           out={k: v[:len(fb)] for k, v in arrays.items()})
-            t_render += time.time() - tr
+                    pose_cache[e] = object_poses(wl.scene, wl.epoch(e).object_frames)
             for k, f in enumerate(fb):
                 V, P, C, cam, aim, q = wl.camera(f)
                 lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
@@ -153,15 +191,21 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 log_args = dict(n_objects=lab["num_objects"], kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
                                 cam_pos=cam, depth_range=out["depth_range"][k].copy() if "depth_range" in out else None)
                 files = []
-                if "rgb" in outs:
+                if kinds:   # GPU-encoded: file j = frame * nk + index of its kind
+                    for o, kd, path in (("rgb", "rgb_png", os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png")),
+                                        ("depth_csv", "depth_csv", os.path.join(out_dir, "depth", f"depth_{f:06d}.csv")),
+                                        ("depth_png", "depth_png", os.path.join(out_dir, "depth", f"depth_{f:06d}.png"))):
+                        if o in outs:
+                            files.append((path, "encoded", (k * nk + kinds.index(kd),)))
+                elif "rgb" in outs:
                     files.append((os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), "png", ("rgb",)))
                 if "mask" in outs:
                     files.append((os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"), "npy", ("instance",)))
                 if "depth_npy" in outs:
                     files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"), "npy", ("depth",)))
-                if "depth_csv" in outs:
+                if "depth_csv" in outs and not kinds:
                     files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), "csv", ("depth",)))
-                if "depth_png" in outs:
+                if "depth_png" in outs and not kinds:
                     files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.png"), "png", ("depth_vis",)))
                 if "pointcloud" in outs:
                     files.append((os.path.join(out_dir, "pointcloud", f"pointcloud_{f:06d}.txt"), "pointcloud",
@@ -170,13 +214,14 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                     files.append((os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), "npy", ("normals",)))
                 fut = pool.submit(slot, k, files, lab, os.path.join(out_dir, "labels", f"label_{f:06d}.json"))
                 pending.append((fut, log_args))
-            del out, arrays
+            del out
             # log frames in order as they complete
             while pending and pending[0][0].done():
                 _log_done(log, *pending.pop(0), "pointcloud" in outs)
         for p in pending:
             _log_done(log, *p, "pointcloud" in outs)
     finally:
+        ahead.shutdown(wait=True)
         pool.close()
         r.close()
     wall = time.time() - t0

@@ -16,7 +16,6 @@ reference numbers visible objects in Replicator's order, unknowable offline).
 """
 from __future__ import annotations
 
-import json
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -100,24 +99,26 @@ def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dic
     """The label JSON of one frame (:2056-2064) for the objects visible in it
     (+ ``occlusion_ratio`` per object when the coverage is given)."""
     occ = occlusion_ratios(inst_stats[:, 0], covered) if inst_stats is not None and covered is not None else None
+    occ = occ.tolist() if occ is not None else None
     objs = []
     kp_by_obj: Dict[int, list] = {}
     if kp_uv is not None and kp_table is not None:
-        for k, (j, name) in enumerate(kp_table):
-            kp_by_obj.setdefault(j, []).append(
-                [name, float(kp_uv[k, 0]), float(kp_uv[k, 1]), int(kp_vis[k])])
+        # (tolist: Python floats / ints of the same values, without a per-element numpy access)
+        for (j, name), (u, v), vis in zip(kp_table, kp_uv.tolist(), kp_vis.tolist()):
+            kp_by_obj.setdefault(j, []).append([name, u, v, vis])
+    stats = inst_stats.tolist() if inst_stats is not None else None
     for j, p in enumerate(poses):
-        if inst_stats is not None:
-            cnt = int(inst_stats[p["inst_idx"], 0]) if p["inst_idx"] < inst_stats.shape[0] else 0
-            if cnt == 0:
+        i = p["inst_idx"]
+        if stats is not None:
+            if i >= len(stats) or stats[i][0] == 0:
                 continue
         e = dict(p)
-        if inst_stats is not None:
-            st = inst_stats[p["inst_idx"]]
-            e["pixel_count"] = int(st[0])
-            e["bbox_2d"] = [int(st[1]), int(st[2]), int(st[3]), int(st[4])]
+        if stats is not None:
+            st = stats[i]
+            e["pixel_count"] = st[0]
+            e["bbox_2d"] = st[1:5]
             if occ is not None:
-                e["occlusion_ratio"] = float(occ[p["inst_idx"]])
+                e["occlusion_ratio"] = occ[i]
         if j in kp_by_obj:
             e["keypoints_2d"] = kp_by_obj[j]
         objs.append(e)
@@ -132,6 +133,31 @@ def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dic
     }
 
 
+_JSON = None
+
+
+def json_encoder():
+    """The native encoder (_csgjson.so, csrc/csg_json.cpp): the bytes of
+    ``json.dumps(obj, indent=2, ensure_ascii=False)``, ~30x faster than the
+    standard library's pure-Python indented encoder; built on first use."""
+    global _JSON
+    if _JSON is None:
+        import importlib
+        from .build import JSON_EXT, JSON_SOURCES, build_json, needs_build
+        if needs_build(JSON_EXT, JSON_SOURCES):
+            build_json()
+        _JSON = importlib.import_module(__package__ + "._csgjson")
+    return _JSON
+
+
+def label_json_bytes(label: dict) -> bytes:
+    """The label file's bytes, exactly as save_label_json (GDP:608-613) writes them."""
+    return json_encoder().dumps_indent2(label)
+
+
 def save_label_json(label: dict, filename: str) -> None:
-    with open(filename, "w", encoding="utf-8") as f:
-        json.dump(label, f, indent=2, ensure_ascii=False)
+    """save_label_json of the reference (GDP:608-613): ``json.dump(indent=2,
+    ensure_ascii=False)`` to a UTF-8 file, through the native encoder."""
+    data = label_json_bytes(label)
+    with open(filename, "wb") as f:
+        f.write(data)

@@ -24,7 +24,8 @@ from .scene.model import Scene
 FRAME_DTYPE = np.dtype([("view", "<f4", 16), ("proj", "<f4", 16), ("xform_set", "<u4"), ("frame_id", "<u4")])
 assert FRAME_DTYPE.itemsize == C.sizeof(_lib.Frame)
 
-OUTPUT_KINDS = ("rgb", "instance", "depth", "keypoints", "stats", "normals", "points", "depth_vis", "covered")
+OUTPUT_KINDS = ("rgb", "instance", "depth", "keypoints", "stats", "normals", "points", "depth_vis", "depth_range",
+                "covered")
 
 
 def make_frames(views: np.ndarray, projs: np.ndarray, sets: Sequence[int], frame_ids: Sequence[int]) -> np.ndarray:
@@ -74,6 +75,7 @@ def output_spec(n: int, H: int, W: int, n_kp: int, n_labels: int, want: Iterable
         spec["points"] = ((n, H, W, 3), np.float32)
     if "depth_vis" in want:   # the reference's JET depth PNG (GDP:1690-1709) and its min / max
         spec["depth_vis"] = ((n, H, W, 3), np.uint8)
+    if "depth_vis" in want or "depth_range" in want:
         spec["depth_range"] = ((n, 2), np.float32)
     if "covered" in want:     # unoccluded pixels per label (occlusionRatio)
         spec["label_covered"] = ((n, n_labels), np.uint32)

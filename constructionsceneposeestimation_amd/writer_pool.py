@@ -47,14 +47,33 @@ def _write_png(path: str, rgb: np.ndarray) -> None:
     fileio.write_png(path, rgb, level=1, strategy="rle")
 
 
+def _write_bytes(path: str, data) -> None:
+    """Write a buffer (os.write releases the GIL)."""
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        mv = memoryview(data)
+        while mv:
+            n = os.write(fd, mv)
+            mv = mv[n:]
+    finally:
+        os.close(fd)
+
+
 def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, str, Tuple[str, ...]]],
                 label: dict, label_path: str) -> Optional[dict]:
     """Every file of frame ``k`` of a batch, then its label JSON (the resume
     marker, GDP:1357-1367 scans labels/).  ``files`` = (path, kind, array
-    names); returns the frame's depth counts for the quality log."""
+    names); kind "encoded" names the file index j in the batch's files
+    encoded on the GPU (arrays "files" + "file_offsets"); returns the frame's
+    depth counts for the quality log."""
     from . import writers as fileio
-    from .labels import save_label_json
+    from .labels import label_json_bytes
     for path, kind, keys in files:
+        if kind == "encoded":
+            off = arrays["file_offsets"]
+            j = keys[0]
+            _atomic(path, _write_bytes, arrays["files"][int(off[j]):int(off[j + 1])])
+            continue
         a = [arrays[x][k] for x in keys]
         if kind == "png":
             _atomic(path, _write_png, *a)
@@ -66,7 +85,7 @@ def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, st
             _atomic(path, fileio.write_pointcloud_txt, *a)
         else:
             raise ValueError(kind)
-    _atomic(label_path, lambda p, lab: save_label_json(lab, p), label)
+    _atomic(label_path, _write_bytes, label_json_bytes(label))
     return fileio.depth_stats(arrays["depth"][k]) if "depth" in arrays else None
 
 
@@ -127,6 +146,20 @@ class WriterPool:
                            for _ in range(n_slots)]
         else:
             raise ValueError(f"writer mode {mode!r}: 'process' or 'thread'")
+
+    def set_files_buffers(self, alloc, nbytes: int) -> None:
+        """Thread mode: give every slot a ``files`` buffer of ``nbytes`` from
+        ``alloc(nbytes)`` (pinned memory of the renderer) for the files the GPU
+        encodes (Renderer.render_files)."""
+        assert self._local is not None, "GPU-encoded files need writer threads"
+        for d in self._local:
+            d["files"] = alloc(nbytes)
+        self.alloc = alloc
+
+    def grow_files(self, slot: int, nbytes: int) -> np.ndarray:
+        """A larger ``files`` buffer for a slot (the batch's files did not fit)."""
+        self._local[slot]["files"] = self.alloc(nbytes)
+        return self._local[slot]["files"]
 
     def arrays(self, slot: int) -> Dict[str, np.ndarray]:
         """The slot's arrays, to render into (waits until no task reads it)."""

@@ -90,3 +90,28 @@ def test_files_buffer_too_small_then_copy():
     wl = Workload("C3", seed=0)
     out, blobs = _render(wl, [1200, 1201], 480, 272, cap=4096)
     _check(out, blobs, 2)
+
+
+def test_generate_gpu_files_match_host_writers(tmp_path):
+    """generate() with writer threads (files encoded on the GPU) against
+    writer processes (the host writers, libcsgio + json): same pixels in
+    every PNG, byte-identical depth CSVs, masks and label JSON."""
+    import os
+
+    from constructionsceneposeestimation_amd.generate import generate
+    kw = dict(workload="C3", seed=2, batch=4, width=200, height=120, writers=2)
+    generate(str(tmp_path / "gpu"), list(range(9)), writer_mode="thread", **kw)
+    generate(str(tmp_path / "host"), list(range(9)), writer_mode="process", **kw)
+    n = 0
+    for sub in ("rgb", "depth", "labels"):
+        names = sorted(os.listdir(tmp_path / "gpu" / sub))
+        assert names == sorted(os.listdir(tmp_path / "host" / sub)) and names
+        for name in names:
+            a = open(tmp_path / "gpu" / sub / name, "rb").read()
+            b = open(tmp_path / "host" / sub / name, "rb").read()
+            if name.endswith(".png"):
+                assert np.array_equal(decode_png(a), decode_png(b)), name
+            else:
+                assert a == b, name
+            n += 1
+    assert n == 9 * 5
