@@ -80,16 +80,25 @@ def bboxDict_to_transform(bbox) -> tuple:
 
 
 def object_poses(scene, object_frames) -> List[dict]:
-    """Pose entries of every object (cache per randomisation epoch)."""
+    """Pose entries of every object (cache per randomisation epoch):
+    bboxDict_to_transform (:553-584) of every record at once (stacked SVD and
+    rotation conversion; the per-record function above is the restatement the
+    golden vectors pin, this agrees with it to ~1e-15)."""
     recs = bbox3d_records(scene, object_frames)
-    out = []
-    for j, o in enumerate(scene.objects):
-        r = recs[j]
-        c, s, e = bboxDict_to_transform((r["semanticId"], r["x_min"], r["y_min"], r["z_min"], r["x_max"],
-                                         r["y_max"], r["z_max"], r["transform"], r["occlusionRatio"]))
-        out.append({"inst_idx": o.inst_idx, "class_id": o.class_id, "class_name": o.class_name,
-                    "center": c, "size": s, "rotation": e, "prim_path": o.prim_path})
-    return out
+    if len(recs) == 0:
+        return []
+    lo = np.stack([recs["x_min"], recs["y_min"], recs["z_min"]], 1).astype(np.float64)
+    hi = np.stack([recs["x_max"], recs["y_max"], recs["z_max"]], 1).astype(np.float64)
+    T = recs["transform"].astype(np.float64).transpose(0, 2, 1)
+    mean = np.concatenate([(lo + hi) / 2.0, np.ones((len(recs), 1))], 1)
+    center = np.einsum("nij,nj->ni", T, mean)[:, :3]
+    rot = T[:, :3, :3]
+    U, _, Vt = np.linalg.svd(rot)
+    euler = Rotation.from_matrix(U @ Vt).as_euler("xyz", degrees=True)
+    size = np.linalg.norm(rot, axis=1) * np.abs(hi - lo)
+    return [{"inst_idx": o.inst_idx, "class_id": o.class_id, "class_name": o.class_name,
+             "center": c, "size": sz, "rotation": e, "prim_path": o.prim_path}
+            for o, c, sz, e in zip(scene.objects, center.tolist(), size.tolist(), euler.tolist())]
 
 
 def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dict, poses: List[dict],

@@ -163,18 +163,22 @@ PRIMITIVES = {
 
 
 def bone_matrix(a: np.ndarray, b: np.ndarray, radius: float) -> np.ndarray:
-    """Unit cylinder (z 0..1) -> cylinder from a to b of the given radius."""
-    d = np.asarray(b, float) - np.asarray(a, float)
-    L = float(np.linalg.norm(d))
-    z = d / L if L > 0 else np.array([0, 0, 1.0])
-    helper = np.array([1.0, 0, 0]) if abs(z[0]) < 0.9 else np.array([0, 1.0, 0])
-    x = np.cross(helper, z)
-    x /= np.linalg.norm(x)
-    y = np.cross(z, x)
-    m = np.eye(4)
-    m[:3, 0], m[:3, 1], m[:3, 2] = x * radius, y * radius, z * L
-    m[:3, 3] = a
-    return m
+    """Unit cylinder (z 0..1) -> cylinder from a to b of the given radius.
+    (Scalar float arithmetic: numpy's per-call overhead on 3-vectors was most
+    of the generator's per-epoch pose time.)"""
+    a0, a1, a2 = (float(v) for v in a)
+    d0, d1, d2 = float(b[0]) - a0, float(b[1]) - a1, float(b[2]) - a2
+    L = math.sqrt(d0 * d0 + d1 * d1 + d2 * d2)
+    z0, z1, z2 = (d0 / L, d1 / L, d2 / L) if L > 0 else (0.0, 0.0, 1.0)
+    h0, h1, h2 = (1.0, 0.0, 0.0) if abs(z0) < 0.9 else (0.0, 1.0, 0.0)
+    x0, x1, x2 = h1 * z2 - h2 * z1, h2 * z0 - h0 * z2, h0 * z1 - h1 * z0     # helper x z
+    n = math.sqrt(x0 * x0 + x1 * x1 + x2 * x2)
+    x0, x1, x2 = x0 / n, x1 / n, x2 / n
+    y0, y1, y2 = z1 * x2 - z2 * x1, z2 * x0 - z0 * x2, z0 * x1 - z1 * x0     # z x x
+    return np.array([[x0 * radius, y0 * radius, z0 * L, a0],
+                     [x1 * radius, y1 * radius, z1 * L, a1],
+                     [x2 * radius, y2 * radius, z2 * L, a2],
+                     [0.0, 0.0, 0.0, 1.0]])
 
 
 def box_matrix(center, size, yaw_pitch: Optional[np.ndarray] = None) -> np.ndarray:

@@ -94,13 +94,22 @@ class Workload:
             for n in COCO_JOINTS:
                 self.kp_table.append((j, n))
         self._epoch_cache: Dict[int, EpochState] = {}
+        self._cam_cache: Dict[int, tuple] = {}
 
     # -- per frame ------------------------------------------------------------
     def camera(self, frame: int):
+        """(V, P, C, cam, aim, q) of a frame; memoised (the generator asks for
+        a frame's camera when it renders it and again for its label)."""
+        hit = self._cam_cache.get(frame)
+        if hit is not None:
+            return hit
         cam, aim = schedule.camera_pose(self.seed, frame)
         q = cm.look_at_world_quat(cam, aim)
         V, P, C = cm.frame_matrices(cam, q, self.intr)
-        return V, P, C, cam, aim, q
+        if len(self._cam_cache) >= 4096:
+            self._cam_cache.clear()
+        self._cam_cache[frame] = out = (V, P, C, cam, aim, q)
+        return out
 
     def frame_params(self, frame_ids) -> Tuple[np.ndarray, np.ndarray]:
         Vs, Ps = [], []
@@ -134,6 +143,8 @@ class Workload:
         st = EpochState(models, frames, np.vstack(kps) if kps else np.zeros((0, 3)), joints)
         if self.dr:
             st.dr = schedule.domain_randomization(self.scene, self.seed, e, self.dr_variants)
+        if len(self._epoch_cache) >= 256:   # bounded: a long run visits each epoch once
+            self._epoch_cache.pop(next(iter(self._epoch_cache)))
         self._epoch_cache[e] = st
         return st
 
