@@ -71,7 +71,8 @@ class Outputs(C.Structure):
                 ("n_labels", C.c_uint32), ("on_device", C.c_int32), ("normals", C.c_void_p),
                 ("points", C.c_void_p), ("depth_vis", C.c_void_p), ("depth_range", C.c_void_p),
                 ("label_covered", C.c_void_p), ("file_kinds", C.c_uint32), ("pad_files", C.c_uint32),
-                ("files", C.c_void_p), ("files_cap", C.c_uint64), ("file_offsets", C.c_void_p)]
+                ("files", C.c_void_p), ("files_cap", C.c_uint64), ("file_offsets", C.c_void_p),
+                ("depth_stats", C.c_void_p)]
 
 
 class BatchStats(C.Structure):

@@ -147,6 +147,8 @@ struct csg_ctx {
   DevBuf<uint32_t> enc_rows_rgb, enc_rows_dpng, enc_rows_csv;
   DevBuf<uint64_t> enc_fsize, enc_foff, enc_zoff;
   DevBuf<uint8_t> enc_zbuf, enc_out;
+  DevBuf<uint8_t> dstat_part;           // depth-statistics partial sums
+  DevBuf<double> o_dstats;              // depth statistics (host-output mode)
   uint64_t enc_total = 0;               // bytes of the last batch's files (0: none)
   uint32_t enc_nfiles = 0;
   std::vector<uint64_t> h_foff;
@@ -793,7 +795,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     HIP_TRY(c, c->o_rgb.alloc(F * npx * 3));
     b.rgb = c->o_rgb.p;
   }
-  if ((fk & CSG_FILE_DEPTH_CSV) && !b.depth) {
+  if ((fk & CSG_FILE_DEPTH_CSV || out->depth_stats) && !b.depth) {
     HIP_TRY(c, c->o_depth.alloc(F * npx));
     b.depth = c->o_depth.p;
   }
@@ -816,6 +818,12 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       if (dev) drange_out = out->depth_range;
       else { HIP_TRY(c, c->o_drange.alloc((size_t)F * 2)); drange_out = c->o_drange.p; }
     }
+  }
+  double* dstats = nullptr;
+  if (out->depth_stats) {
+    HIP_TRY(c, c->dstat_part.alloc(depth_stats_scratch_bytes(c->chain_frames)));
+    if (dev) dstats = out->depth_stats;
+    else { HIP_TRY(c, c->o_dstats.alloc((size_t)F * 6)); dstats = c->o_dstats.p; }
   }
   b.tile_words = (c->n_tiles + 31u) / 32u;
   if (want_kp) {
@@ -875,6 +883,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[3], st));
     launch_raster(s, bc, Fc, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[4], st));
+    if (out->depth_stats)
+      launch_depth_stats(bc.depth, (uint32_t)npx, Fc, c->dstat_part.p, dstats + (size_t)c0 * 6, st);
     if (want_dvis) {
       launch_depth_range(bc.depth, (uint32_t)npx, Fc, c->drange.p, st);
       if (dvis || drange_out) {
@@ -901,6 +911,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       HIP_TRY(c, hipMemcpyAsync(out->label_covered, b.covered, (size_t)F * out->n_labels * 4, hipMemcpyDeviceToHost, st));
     if (out->depth_vis) HIP_TRY(c, hipMemcpyAsync(out->depth_vis, dvis, F * npx * 3, hipMemcpyDeviceToHost, st));
     if (drange_out) HIP_TRY(c, hipMemcpyAsync(out->depth_range, drange_out, (size_t)F * 8, hipMemcpyDeviceToHost, st));
+    if (dstats) HIP_TRY(c, hipMemcpyAsync(out->depth_stats, dstats, (size_t)F * 48, hipMemcpyDeviceToHost, st));
     if (want_kp && out->keypoints_uv)
       HIP_TRY(c, hipMemcpyAsync(out->keypoints_uv, b.kp_uv, (size_t)F * c->n_kp * 8, hipMemcpyDeviceToHost, st));
     if (want_kp && out->keypoints_vis)

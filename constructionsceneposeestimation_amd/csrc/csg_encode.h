@@ -33,4 +33,9 @@ void launch_png_emit(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, con
 void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,
                      const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st);
 
+// Quality-log depth statistics of F frames: out [F][6] (csg_outputs.depth_stats);
+// scratch of depth_stats_scratch_bytes(F).
+size_t depth_stats_scratch_bytes(uint32_t F);
+void launch_depth_stats(const float* depth, uint32_t npx, uint32_t F, void* scratch, double* out, hipStream_t st);
+
 }  // namespace csg

@@ -544,6 +544,74 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_csv_emit(const float* __restr
   o.finish();
 }
 
+// ---------------------------------------------------------------------------
+// depth statistics of the quality log (csg_outputs.depth_stats)
+// ---------------------------------------------------------------------------
+constexpr uint32_t kStatBlocks = 64;
+struct DepthPartial {
+  double sum;
+  uint32_t valid, zero, inf, mn, mx, pad;
+};
+
+__global__ __launch_bounds__(256) void k_depth_stats(const float* __restrict__ depth, uint32_t npx,
+                                                     DepthPartial* __restrict__ part) {
+  const uint32_t f = blockIdx.y;
+  const float* d = depth + (size_t)f * npx;
+  double sum = 0.0;
+  uint32_t valid = 0, zero = 0, inf = 0, mn = 0xFFFFFFFFu, mx = 0u;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < npx; i += kStatBlocks * 256u) {
+    const float v = d[i];
+    const uint32_t u = __float_as_uint(v);
+    if (v > 0.0f && v < INFINITY) {
+      ++valid;
+      sum += (double)v;
+      mn = min(mn, u);
+      mx = max(mx, u);
+    }
+    zero += v == 0.0f ? 1u : 0u;
+    inf += (u & 0x7FFFFFFFu) == 0x7F800000u ? 1u : 0u;
+  }
+  __shared__ DepthPartial sh[256];
+  sh[threadIdx.x] = DepthPartial{sum, valid, zero, inf, mn, mx, 0};
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {   // fixed tree order: deterministic
+    if (threadIdx.x < o) {
+      DepthPartial& a = sh[threadIdx.x];
+      const DepthPartial& b = sh[threadIdx.x + o];
+      a.sum += b.sum;
+      a.valid += b.valid;
+      a.zero += b.zero;
+      a.inf += b.inf;
+      a.mn = min(a.mn, b.mn);
+      a.mx = max(a.mx, b.mx);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[(size_t)f * kStatBlocks + blockIdx.x] = sh[0];
+}
+
+__global__ void k_depth_stats_final(const DepthPartial* __restrict__ part, uint32_t F, double* __restrict__ out) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  DepthPartial a{0.0, 0, 0, 0, 0xFFFFFFFFu, 0u, 0};
+  for (uint32_t b = 0; b < kStatBlocks; ++b) {
+    const DepthPartial& p = part[(size_t)f * kStatBlocks + b];
+    a.sum += p.sum;
+    a.valid += p.valid;
+    a.zero += p.zero;
+    a.inf += p.inf;
+    a.mn = min(a.mn, p.mn);
+    a.mx = max(a.mx, p.mx);
+  }
+  double* o = out + (size_t)f * 6;
+  o[0] = a.valid;
+  o[1] = a.zero;
+  o[2] = a.inf;
+  o[3] = a.sum;
+  o[4] = a.valid ? (double)__uint_as_float(a.mn) : 0.0;
+  o[5] = a.valid ? (double)__uint_as_float(a.mx) : 0.0;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -582,6 +650,14 @@ void launch_png_emit(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, con
   const uint32_t max_ch = (uint32_t)((max_z + kIdatBytes - 1) / kIdatBytes);
   hipLaunchKernelGGL(k_png_pack, dim3((max_ch + 63) / 64, F), dim3(64), 0, st, png, zbuf, zbase, out, foff, W, H, nk,
                      kslot);
+}
+
+size_t depth_stats_scratch_bytes(uint32_t F) { return sizeof(DepthPartial) * kStatBlocks * F; }
+
+void launch_depth_stats(const float* depth, uint32_t npx, uint32_t F, void* scratch, double* out, hipStream_t st) {
+  DepthPartial* part = static_cast<DepthPartial*>(scratch);
+  hipLaunchKernelGGL(k_depth_stats, dim3(kStatBlocks, F), dim3(256), 0, st, depth, npx, part);
+  hipLaunchKernelGGL(k_depth_stats_final, dim3((F + 63) / 64), dim3(64), 0, st, part, F, out);
 }
 
 void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,

@@ -61,7 +61,9 @@ def default_writers() -> int:
 
 
 def _log_done(log: QualityLog, fut, log_args: dict, points: bool) -> None:
-    ds = fut.result()
+    ds = fut.result()                       # host depth counts (writer), else the GPU's
+    gpu_ds = log_args.pop("gpu_depth_stats", None)
+    ds = ds if ds is not None else gpu_ds
     log.frame(depth_stats=ds, points=ds["valid"] if points and ds else None, **log_args)
 
 
@@ -115,11 +117,12 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     gpu_files = writer_mode == "thread"
     kinds = tuple(k for o, k in (("rgb", "rgb_png"), ("depth_csv", "depth_csv"), ("depth_png", "depth_png"))
                   if o in outs) if gpu_files else ()
-    # host depth: for its own files, and for the quality log's depth counts
-    host_depth = bool(outs & {"depth_npy", "pointcloud", "depth_csv"})
+    # host depth for its own files; the quality log's depth counts come from
+    # the GPU (depth_stats) in thread mode, from the host depth otherwise
+    host_depth = bool(outs & {"depth_npy", "pointcloud"}) or (not gpu_files and "depth_csv" in outs)
     log = QualityLog(os.path.join(out_dir, "logs"))
     if gpu_files:
-        want = (["keypoints", "stats", "covered"] + (["instance"] if "mask" in outs else [])
+        want = (["keypoints", "stats", "covered", "depth_stats"] + (["instance"] if "mask" in outs else [])
                 + (["depth"] if host_depth else []) + (["depth_range"] if "depth_png" in outs else [])
                 + (["points", "rgb"] if "pointcloud" in outs else []) + (["normals"] if "normals" in outs else []))
     else:
@@ -131,10 +134,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     pool = WriterPool(output_spec(batch, wl.height, wl.width, wl.n_keypoints(), scene_labels(wl.scene), want),
                       n_writers, n_slots=3, mode=writer_mode)
     r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
-    if kinds:   # pinned buffers for the encoded files: a generous estimate, grown on demand
+    if gpu_files:   # page-locked slots, and buffers for the encoded files (an estimate, grown on demand)
         npx = wl.width * wl.height
         est = {"rgb_png": 2 * npx, "depth_csv": 10 * npx, "depth_png": npx}
-        pool.set_files_buffers(r.host_buffer, batch * sum(est[k] for k in kinds) + (1 << 20))
+        pool.use_pinned(r.host_buffer, batch * sum(est[k] for k in kinds) + (1 << 20) if kinds else 0)
     nk = len(kinds)
     intr = wl.intr
     pose_cache = {}
@@ -190,6 +193,11 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                                    wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k])
                 log_args = dict(n_objects=lab["num_objects"], kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
                                 cam_pos=cam, depth_range=out["depth_range"][k].copy() if "depth_range" in out else None)
+                if "depth_stats" in out:   # valid, zero, inf, sum, min, max (csg_outputs.depth_stats)
+                    v = out["depth_stats"][k].tolist()
+                    log_args["gpu_depth_stats"] = {"valid": int(v[0]), "zero": int(v[1]), "inf": int(v[2]),
+                                                   "total": wl.width * wl.height, "sum": v[3], "min": v[4],
+                                                   "max": v[5]}
                 files = []
                 if kinds:   # GPU-encoded: file j = frame * nk + index of its kind
                     for o, kd, path in (("rgb", "rgb_png", os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png")),

@@ -25,7 +25,7 @@ FRAME_DTYPE = np.dtype([("view", "<f4", 16), ("proj", "<f4", 16), ("xform_set", 
 assert FRAME_DTYPE.itemsize == C.sizeof(_lib.Frame)
 
 OUTPUT_KINDS = ("rgb", "instance", "depth", "keypoints", "stats", "normals", "points", "depth_vis", "depth_range",
-                "covered")
+                "covered", "depth_stats")
 
 
 def make_frames(views: np.ndarray, projs: np.ndarray, sets: Sequence[int], frame_ids: Sequence[int]) -> np.ndarray:
@@ -77,6 +77,8 @@ def output_spec(n: int, H: int, W: int, n_kp: int, n_labels: int, want: Iterable
         spec["depth_vis"] = ((n, H, W, 3), np.uint8)
     if "depth_vis" in want or "depth_range" in want:
         spec["depth_range"] = ((n, 2), np.float32)
+    if "depth_stats" in want:   # the quality log's depth counts: valid, zero, inf, sum, min, max
+        spec["depth_stats"] = ((n, 6), np.float64)
     if "covered" in want:     # unoccluded pixels per label (occlusionRatio)
         spec["label_covered"] = ((n, n_labels), np.uint32)
     return spec
@@ -219,7 +221,7 @@ class Renderer:
                               ("keypoints_uv", "keypoints_uv"), ("keypoints_vis", "keypoints_vis"),
                               ("inst_stats", "inst_stats"), ("normals", "normals"), ("points", "points"),
                               ("depth_vis", "depth_vis"), ("depth_range", "depth_range"),
-                              ("label_covered", "label_covered")):
+                              ("label_covered", "label_covered"), ("depth_stats", "depth_stats")):
                 arr = out.get(key)
                 if arr is not None:
                     setattr(oo, name, arr[s:e].ctypes.data)
@@ -273,7 +275,7 @@ class Renderer:
             raise CsgError("render_files: files must be a C-contiguous uint8 array")
         oo = _lib.Outputs()
         for key in ("rgb", "instance", "depth", "keypoints_uv", "keypoints_vis", "inst_stats", "normals", "points",
-                    "depth_vis", "depth_range", "label_covered"):
+                    "depth_vis", "depth_range", "label_covered", "depth_stats"):
             arr = out.get(key)
             if arr is not None:
                 setattr(oo, key, arr.ctypes.data)
@@ -296,11 +298,11 @@ class Renderer:
     def render_into(self, frames_ptr: int, n: int, frames_on_device: bool, rgb: int = 0, instance: int = 0,
                     depth: int = 0, kp_uv: int = 0, kp_vis: int = 0, stats: int = 0, stream: int = 0,
                     normals: int = 0, points: int = 0, depth_vis: int = 0, depth_range: int = 0,
-                    covered: int = 0) -> None:
+                    covered: int = 0, depth_stats: int = 0) -> None:
         """Enqueue a batch writing device buffers (raw pointers, e.g. torch ``data_ptr()``)."""
         o = _lib.Outputs(rgb or None, instance or None, depth or None, kp_uv or None, kp_vis or None,
                          stats or None, self.n_labels, 1, normals or None, points or None, depth_vis or None,
-                         depth_range or None, covered or None, 0, 0, None, 0, None)
+                         depth_range or None, covered or None, 0, 0, None, 0, None, depth_stats or None)
         self._check(self.lib.csg_render_batch_async(self.ctx, frames_ptr, n, int(frames_on_device), C.byref(o),
                                                     stream or None), "render_batch_async")
 

@@ -147,13 +147,19 @@ class WriterPool:
         else:
             raise ValueError(f"writer mode {mode!r}: 'process' or 'thread'")
 
-    def set_files_buffers(self, alloc, nbytes: int) -> None:
-        """Thread mode: give every slot a ``files`` buffer of ``nbytes`` from
-        ``alloc(nbytes)`` (pinned memory of the renderer) for the files the GPU
-        encodes (Renderer.render_files)."""
-        assert self._local is not None, "GPU-encoded files need writer threads"
-        for d in self._local:
-            d["files"] = alloc(nbytes)
+    def use_pinned(self, alloc, files_bytes: int = 0) -> None:
+        """Thread mode: the slots' arrays in page-locked memory from
+        ``alloc(nbytes)`` (Renderer.host_buffer: device-to-host copies at full
+        PCIe rate), plus a ``files`` buffer of ``files_bytes`` per slot for the
+        files the GPU encodes (Renderer.render_files)."""
+        assert self._local is not None, "pinned slots need writer threads"
+        for slot in range(self.n_slots):
+            buf = alloc(self.slot_bytes)
+            d = {k: np.ndarray(shape, np.dtype(dt), buffer=buf, offset=off)
+                 for k, (off, shape, dt) in self.layout.items()}
+            if files_bytes:
+                d["files"] = alloc(files_bytes)
+            self._local[slot] = d
         self.alloc = alloc
 
     def grow_files(self, slot: int, nbytes: int) -> np.ndarray:

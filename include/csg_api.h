@@ -146,6 +146,10 @@ typedef struct {
   uint8_t* files;
   uint64_t files_cap;
   uint64_t* file_offsets;
+  double* depth_stats;       /* [n][6] per frame: valid pixels (finite, > 0), zero pixels, infinite
+                                pixels, sum / min / max of the valid depths (the reference's
+                                DataQualityLogger.log_depth, GDP:318-341); the sum in float64 in a
+                                fixed order (64 partial sums per frame, then in order) */
 } csg_outputs;
 
 /* csg_outputs.file_kinds */
