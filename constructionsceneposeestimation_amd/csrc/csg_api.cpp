@@ -959,7 +959,7 @@ static int encode_files(csg_ctx* c, const csg_outputs* out, uint32_t F) {
   if (fk & CSG_FILE_DEPTH_PNG) slot_dpng = nk++;
   const uint32_t W = c->cfg.width, H = c->cfg.height, n_files = F * nk;
   hipStream_t st = c->stream;
-  const size_t rows = (size_t)F * H;
+  const size_t rows = (size_t)F * png_units_per_frame(W, H), csv_rows = (size_t)F * csv_units_per_frame(W, H);
   HIP_TRY(c, c->enc_fsize.alloc(n_files));
   HIP_TRY(c, c->enc_foff.alloc(n_files + 1));
   HIP_TRY(c, c->enc_zoff.alloc(2 * (size_t)F + 1));
@@ -977,7 +977,7 @@ static int encode_files(csg_ctx* c, const csg_outputs* out, uint32_t F) {
                      slot_dpng, st);
   }
   if (fk & CSG_FILE_DEPTH_CSV) {
-    HIP_TRY(c, c->enc_rows_csv.alloc(rows));
+    HIP_TRY(c, c->enc_rows_csv.alloc(csv_rows));
     launch_csv_sizes(c->last_depth, W, H, F, c->enc_rows_csv.p, c->enc_fsize.p, nk, slot_csv, st);
   }
   const EncPng* pa = (fk & CSG_FILE_RGB_PNG) ? c->enc_rgb.p : nullptr;

@@ -16,11 +16,14 @@ struct EncPng {
   uint32_t hdr_bits, adler, eob_pos, zbytes;  // zbytes: the zlib stream incl. the Adler-32
 };
 
+// Work units per frame (segments of rows): scratch arrays are [F][units].
+uint32_t png_units_per_frame(uint32_t W, uint32_t H);
+uint32_t csv_units_per_frame(uint32_t W, uint32_t H);
 // Passes up to the sizes: fsize[f * nk + kslot] = PNG file bytes of frame f.
-// rowsum [F][H], rowbits [F][H] scratch (rowbits become the row bit offsets).
+// rowsum, rowbits: [F][png units] scratch (rowbits become the units' bit offsets).
 void launch_png_sizes(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, EncPng* png, uint2* rowsum,
                       uint32_t* rowbits, uint64_t* fsize, uint32_t nk, uint32_t kslot, hipStream_t st);
-// rowlen [F][H] scratch (becomes the row byte offsets); fsize as above.
+// rowlen [F][csv units] scratch (becomes the units' byte offsets); fsize as above.
 void launch_csv_sizes(const float* depth, uint32_t W, uint32_t H, uint32_t F, uint32_t* rowlen, uint64_t* fsize,
                       uint32_t nk, uint32_t kslot, hipStream_t st);
 // foff[n_files + 1]; zoff[2F + 1] staging offsets of the PNG frames of kind a then kind b (either may be NULL).

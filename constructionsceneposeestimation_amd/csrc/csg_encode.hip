@@ -4,7 +4,8 @@
 // :1672-1673, :1690-1709) and the depth CSV (np.savetxt "%.6f" :1687-1688).
 // The host then only copies the packed bytes out and writes them.
 //
-// Work is parallel over image rows (one thread per row of one frame):
+// Work is parallel over segments of image rows (one thread per 512 bytes of a
+// PNG row stream, per 64 values of a CSV row):
 //
 //   PNG, per image kind (csg_deflate.h for the formats):
 //     k_png_scan    Sub-filter the row on the fly, run-length tokens -> the
@@ -46,36 +47,58 @@ using namespace dfl;
 
 namespace {
 
-constexpr int kRowsPerBlock = 64;   // one wave of rows per workgroup (one frame per workgroup)
+constexpr int kRowsPerBlock = 64;   // one wave of units per workgroup (one frame per workgroup)
+// Work units: segments of rows, so that a batch offers tens of thousands of
+// threads (one thread per 1080p row left the GPU mostly idle).
+constexpr uint32_t kSegBytes = 512;  // PNG: filtered-stream bytes per unit
+constexpr uint32_t kSegVals = 64;    // CSV: values per unit
 
-// Filtered PNG row stream of an 8-bit RGB image row: filter byte 1 (Sub),
-// then each byte minus the byte one pixel (3 bytes) to the left.
+__host__ __device__ __forceinline__ uint32_t png_units(uint32_t W) { return (3u * W + 1u + kSegBytes - 1u) / kSegBytes; }
+__host__ __device__ __forceinline__ uint32_t csv_units(uint32_t W) { return (W + kSegVals - 1u) / kSegVals; }
+
+// Bytes [s0, s1) of the filtered PNG stream of an 8-bit RGB image row
+// (byte 0: filter type 1 = Sub; byte i > 0: raw[i - 1] - raw[i - 4], the
+// byte one pixel to the left, 0 before the row).  Units of kSegBytes of this
+// stream are tokenised independently: a run never crosses a unit boundary
+// (a literal starts each unit; valid deflate, a few bytes larger).
 template <class Sink>
-__device__ __forceinline__ void png_row_bytes(const uint8_t* row, uint32_t W, Sink& sink) {
-  sink.push(1u);
-  const uint32_t n = 3u * W;
-  uint32_t h0 = 0, h1 = 0, h2 = 0;   // raw bytes i-3, i-2, i-1
-  const uintptr_t a = reinterpret_cast<uintptr_t>(row);
-  uint32_t i = 0;
-  // head bytes up to a dword boundary, dwords, tail bytes
-  auto one = [&](uint32_t x) {
-    sink.push((x - h0) & 255u);
-    h0 = h1;
-    h1 = h2;
-    h2 = x;
-  };
-  while (i < n && ((a + i) & 3u)) one(row[i++]);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(row + i);
-  const uint32_t nw = (n - i) >> 2;
-  for (uint32_t k = 0; k < nw; ++k) {
-    const uint32_t v = w[k];
-    one(v & 255u);
-    one((v >> 8) & 255u);
-    one((v >> 16) & 255u);
-    one(v >> 24);
+__device__ __forceinline__ void png_seg_bytes(const uint8_t* row, uint32_t s0, uint32_t s1, Sink& sink) {
+  uint32_t i = s0;
+  if (i == 0) {
+    sink.push(1u);
+    ++i;
   }
-  i += nw * 4u;
-  while (i < n) one(row[i++]);
+  // raw bytes j = i - 1 .. s1 - 2, each minus raw[j - 3]; dword loads where aligned
+  const uintptr_t base = reinterpret_cast<uintptr_t>(row);
+  for (; i < s1 && ((base + i - 1) & 3u); ++i) {
+    const uint32_t j = i - 1;
+    sink.push((uint32_t)(row[j] - (j >= 3 ? row[j - 3] : 0)) & 255u);
+  }
+  uint32_t prev = 0;   // the dword before the current one (bytes j - 4 .. j - 1)
+  if (i < s1 && i - 1 >= 4) prev = *reinterpret_cast<const uint32_t*>(row + i - 5);
+  else if (i < s1) {
+    for (uint32_t k = 0; k < 4; ++k) {
+      const int j = (int)i - 5 + (int)k;
+      prev |= (j >= 0 ? (uint32_t)row[j] : 0u) << (8 * k);
+    }
+  }
+  for (; i + 4 <= s1; i += 4) {
+    const uint32_t cur = *reinterpret_cast<const uint32_t*>(row + i - 1);
+    // left neighbours (3 bytes back) of the 4 bytes of cur: bytes 1..3 of prev, byte 0 of cur
+    const uint32_t left = (prev >> 8) | (cur << 24);
+    const uint32_t jl = i - 1;   // raw index of cur's byte 0 (left valid from raw index 3)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t b = (cur >> (8 * k)) & 255u;
+      const uint32_t l = jl + (uint32_t)k >= 3u ? (left >> (8 * k)) & 255u : 0u;
+      sink.push((b - l) & 255u);
+    }
+    prev = cur;
+  }
+  for (; i < s1; ++i) {
+    const uint32_t j = i - 1;
+    sink.push((uint32_t)(row[j] - (j >= 3 ? row[j - 3] : 0)) & 255u);
+  }
 }
 
 // Adler sums of a byte stream starting from (0, 0), reduced lazily.
@@ -96,13 +119,22 @@ struct AdlerSums {
 // ---------------------------------------------------------------------------
 // PNG pass 1: histogram + Adler sums
 // ---------------------------------------------------------------------------
+// Unit u of a frame: row u / U, stream bytes [(u % U) * kSegBytes, ...).
+__device__ __forceinline__ void png_unit(uint32_t u, uint32_t W, uint32_t U, uint32_t& r, uint32_t& s0, uint32_t& s1) {
+  r = u / U;
+  s0 = (u - r * U) * kSegBytes;
+  s1 = min(s0 + kSegBytes, 3u * W + 1u);
+}
+
 __global__ __launch_bounds__(kRowsPerBlock) void k_png_scan(const uint8_t* __restrict__ img, uint32_t W, uint32_t H,
-                                                            EncPng* __restrict__ png, uint2* __restrict__ rowsum) {
+                                                            EncPng* __restrict__ png, uint2* __restrict__ usum) {
   __shared__ uint32_t hist[kLitCodes];
-  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  const uint32_t f = blockIdx.y, U = png_units(W), u = blockIdx.x * kRowsPerBlock + threadIdx.x;
   for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) hist[s] = 0;
   __syncthreads();
-  if (r < H) {
+  if (u < H * U) {
+    uint32_t r, s0, s1;
+    png_unit(u, W, U, r, s0, s1);
     AdlerSums ad;
     auto lit = [&](uint32_t b) { atomicAdd(&hist[b], 1u); };
     auto match = [&](uint32_t len) {
@@ -118,9 +150,9 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_scan(const uint8_t* __res
         tok.push(x);
       }
     } sink{{lit, match}, &ad};
-    png_row_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, sink);
+    png_seg_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, s0, s1, sink);
     sink.tok.finish();
-    rowsum[(size_t)f * H + r] = make_uint2((uint32_t)(ad.a % kAdlerMod), (uint32_t)(ad.b % kAdlerMod));
+    usum[(size_t)f * H * U + u] = make_uint2((uint32_t)(ad.a % kAdlerMod), (uint32_t)(ad.b % kAdlerMod));
   }
   __syncthreads();
   for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock)
@@ -206,14 +238,39 @@ __global__ __launch_bounds__(256) void k_png_codes(EncPng* __restrict__ png, con
     }
     P.hdr_bits = bb.nbits;
     for (uint32_t s = 0; s < (uint32_t)kLitCodes; ++s) P.code[s] = code[s];
-    // Adler-32 of the whole filtered stream: rows in order from (1, 0)
-    uint32_t a = 1, b = 0;
-    const uint64_t rl = 3ull * W + 1ull;
-    for (uint32_t r = 0; r < H; ++r) {
-      const uint2 v = rowsum[(size_t)f * H + r];
-      adler_cat(a, b, v.x, v.y, rl);
+  }
+  // Adler-32 of the whole filtered stream: each thread folds a contiguous run
+  // of units in order, then an ordered tree over the threads (the fold of
+  // (a, b, length) is associative)
+  __shared__ uint32_t sa[256], sb[256];
+  __shared__ uint64_t sl[256];
+  const uint32_t U = png_units(W), n = H * U, per = (n + 255u) / 256u, lo = t * per, hi = min(n, lo + per);
+  uint32_t a = 0, b = 0;
+  uint64_t l = 0;
+  for (uint32_t u = lo; u < hi; ++u) {
+    const uint2 v = rowsum[(size_t)f * n + u];
+    const uint32_t s0 = (u % U) * kSegBytes, len = min(s0 + kSegBytes, 3u * W + 1u) - s0;
+    adler_cat(a, b, v.x, v.y, len);
+    l += len;
+  }
+  sa[t] = a;
+  sb[t] = b;
+  sl[t] = l;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256u; o <<= 1) {
+    if ((t & (2u * o - 1u)) == 0 && t + o < 256u) {
+      uint32_t a1 = sa[t], b1 = sb[t];
+      adler_cat(a1, b1, sa[t + o], sb[t + o], sl[t + o]);
+      sa[t] = a1;
+      sb[t] = b1;
+      sl[t] += sl[t + o];
     }
-    P.adler = (b << 16) | a;
+    __syncthreads();
+  }
+  if (t == 0) {
+    uint32_t A = 1, B = 0;   // the stream's Adler-32 starts from (1, 0)
+    adler_cat(A, B, sa[0], sb[0], sl[0]);
+    P.adler = (B << 16) | A;
   }
 }
 
@@ -221,12 +278,14 @@ __global__ __launch_bounds__(256) void k_png_codes(EncPng* __restrict__ png, con
 // PNG pass 3: bits per row
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kRowsPerBlock) void k_png_bits(const uint8_t* __restrict__ img, uint32_t W, uint32_t H,
-                                                            const EncPng* __restrict__ png, uint32_t* __restrict__ rowbits) {
+                                                            const EncPng* __restrict__ png, uint32_t* __restrict__ ubits) {
   __shared__ uint8_t clen[kLitCodes];
-  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  const uint32_t f = blockIdx.y, U = png_units(W), u = blockIdx.x * kRowsPerBlock + threadIdx.x;
   for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) clen[s] = (uint8_t)(png[f].code[s] >> 16);
   __syncthreads();
-  if (r >= H) return;
+  if (u >= H * U) return;
+  uint32_t r, s0, s1;
+  png_unit(u, W, U, r, s0, s1);
   uint32_t bits = 0;
   auto lit = [&](uint32_t b) { bits += clen[b]; };
   auto match = [&](uint32_t len) {
@@ -238,9 +297,9 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_bits(const uint8_t* __res
     RunTokenizer<decltype(lit)&, decltype(match)&> tok;
     __device__ void push(uint32_t x) { tok.push(x); }
   } sink{{lit, match}};
-  png_row_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, sink);
+  png_seg_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, s0, s1, sink);
   sink.tok.finish();
-  rowbits[(size_t)f * H + r] = bits;
+  ubits[(size_t)f * H * U + u] = bits;
 }
 
 // exclusive scan of n values (in place) over a 256-thread block; returns the total
@@ -270,12 +329,12 @@ __device__ uint32_t block_scan_inplace(uint32_t* v, uint32_t n, uint32_t* sh) {
 // ---------------------------------------------------------------------------
 // PNG pass 4: row offsets, sizes
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_png_layout(EncPng* __restrict__ png, uint32_t* __restrict__ rowbits, uint32_t H,
+__global__ __launch_bounds__(256) void k_png_layout(EncPng* __restrict__ png, uint32_t* __restrict__ ubits, uint32_t n,
                                                     uint64_t* __restrict__ fsize, uint32_t nk, uint32_t kslot) {
   __shared__ uint32_t sh[256];
   const uint32_t f = blockIdx.x;
   EncPng& P = png[f];
-  const uint32_t total = block_scan_inplace(rowbits + (size_t)f * H, H, sh);
+  const uint32_t total = block_scan_inplace(ubits + (size_t)f * n, n, sh);
   if (threadIdx.x == 0) {
     const uint32_t eob_len = P.code[kEob] >> 16;
     P.eob_pos = P.hdr_bits + total;
@@ -289,22 +348,25 @@ __global__ __launch_bounds__(256) void k_png_layout(EncPng* __restrict__ png, ui
 // ---------------------------------------------------------------------------
 // CSV passes
 // ---------------------------------------------------------------------------
+// Unit u of a frame: row u / V, values [(u % V) * kSegVals, ...), each followed
+// by a space, the row's last by a newline.
 __global__ __launch_bounds__(kRowsPerBlock) void k_csv_len(const float* __restrict__ depth, uint32_t W, uint32_t H,
-                                                           uint32_t* __restrict__ rowlen) {
-  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
-  if (r >= H) return;
+                                                           uint32_t* __restrict__ ulen) {
+  const uint32_t f = blockIdx.y, V = csv_units(W), u = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  if (u >= H * V) return;
+  const uint32_t r = u / V, x0 = (u - r * V) * kSegVals, x1 = min(x0 + kSegVals, W);
   const float* row = depth + ((size_t)f * H + r) * W;
-  uint32_t n = W;   // W - 1 spaces and the newline
+  uint32_t n = x1 - x0;   // separators
   char tmp[kMaxF6Chars];
-  for (uint32_t x = 0; x < W; ++x) n += (uint32_t)fmt6f(row[x], tmp);
-  rowlen[(size_t)f * H + r] = n;
+  for (uint32_t x = x0; x < x1; ++x) n += (uint32_t)fmt6f(row[x], tmp);
+  ulen[(size_t)f * H * V + u] = n;
 }
 
-__global__ __launch_bounds__(256) void k_csv_layout(uint32_t* __restrict__ rowlen, uint32_t H, uint64_t* __restrict__ fsize,
+__global__ __launch_bounds__(256) void k_csv_layout(uint32_t* __restrict__ ulen, uint32_t n, uint64_t* __restrict__ fsize,
                                                     uint32_t nk, uint32_t kslot) {
   __shared__ uint32_t sh[256];
   const uint32_t f = blockIdx.x;
-  const uint32_t total = block_scan_inplace(rowlen + (size_t)f * H, H, sh);
+  const uint32_t total = block_scan_inplace(ulen + (size_t)f * n, n, sh);
   if (threadIdx.x == 0) fsize[(size_t)f * nk + kslot] = total;
 }
 
@@ -368,16 +430,18 @@ struct WordBits {
 
 __global__ __launch_bounds__(kRowsPerBlock) void k_png_emit(const uint8_t* __restrict__ img, uint32_t W, uint32_t H,
                                                             const EncPng* __restrict__ png,
-                                                            const uint32_t* __restrict__ rowoff, uint8_t* zbuf,
+                                                            const uint32_t* __restrict__ uoff, uint8_t* zbuf,
                                                             const uint64_t* __restrict__ zbase) {
   __shared__ uint32_t code[kLitCodes];
-  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  const uint32_t f = blockIdx.y, U = png_units(W), u = blockIdx.x * kRowsPerBlock + threadIdx.x;
   for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) code[s] = png[f].code[s];
   __syncthreads();
-  if (r >= H) return;
+  if (u >= H * U) return;
+  uint32_t r, s0, s1;
+  png_unit(u, W, U, r, s0, s1);
   uint32_t* words = reinterpret_cast<uint32_t*>(zbuf + zbase[f]);
   WordBits wb;
-  wb.init(words, png[f].hdr_bits + rowoff[(size_t)f * H + r]);
+  wb.init(words, png[f].hdr_bits + uoff[(size_t)f * H * U + u]);
   auto lit = [&](uint32_t b) { wb.put(code[b] & 0xFFFFu, code[b] >> 16); };
   auto match = [&](uint32_t len) {
     uint32_t sym, ne, ex;
@@ -390,7 +454,7 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_emit(const uint8_t* __res
     RunTokenizer<decltype(lit)&, decltype(match)&> tok;
     __device__ void push(uint32_t x) { tok.push(x); }
   } sink{{lit, match}};
-  png_row_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, sink);
+  png_seg_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, s0, s1, sink);
   sink.tok.finish();
   wb.finish();
 }
@@ -527,16 +591,17 @@ __global__ __launch_bounds__(64) void k_png_pack(const EncPng* __restrict__ png,
 }
 
 __global__ __launch_bounds__(kRowsPerBlock) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
-                                                            const uint32_t* __restrict__ rowoff, uint8_t* out,
+                                                            const uint32_t* __restrict__ uoff, uint8_t* out,
                                                             const uint64_t* __restrict__ foff, uint32_t nk,
                                                             uint32_t kslot) {
-  const uint32_t f = blockIdx.y, r = blockIdx.x * kRowsPerBlock + threadIdx.x;
-  if (r >= H) return;
+  const uint32_t f = blockIdx.y, V = csv_units(W), u = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  if (u >= H * V) return;
+  const uint32_t r = u / V, x0 = (u - r * V) * kSegVals, x1 = min(x0 + kSegVals, W);
   const float* row = depth + ((size_t)f * H + r) * W;
   ByteOut o;
-  o.init(out, foff[(size_t)f * nk + kslot] + rowoff[(size_t)f * H + r]);
+  o.init(out, foff[(size_t)f * nk + kslot] + uoff[(size_t)f * H * V + u]);
   char tmp[kMaxF6Chars];
-  for (uint32_t x = 0; x < W; ++x) {
+  for (uint32_t x = x0; x < x1; ++x) {
     const int n = fmt6f(row[x], tmp);
     for (int k = 0; k < n; ++k) o.put((uint8_t)tmp[k]);
     o.put(x + 1u < W ? ' ' : '\n');
@@ -617,21 +682,26 @@ __global__ void k_depth_stats_final(const DepthPartial* __restrict__ part, uint3
 // ---------------------------------------------------------------------------
 // launchers (csg_encode.h)
 // ---------------------------------------------------------------------------
-void launch_png_sizes(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, EncPng* png, uint2* rowsum,
-                      uint32_t* rowbits, uint64_t* fsize, uint32_t nk, uint32_t kslot, hipStream_t st) {
-  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
+uint32_t png_units_per_frame(uint32_t W, uint32_t H) { return png_units(W) * H; }
+uint32_t csv_units_per_frame(uint32_t W, uint32_t H) { return csv_units(W) * H; }
+
+void launch_png_sizes(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, EncPng* png, uint2* usum,
+                      uint32_t* ubits, uint64_t* fsize, uint32_t nk, uint32_t kslot, hipStream_t st) {
+  const uint32_t n = png_units_per_frame(W, H);
+  const dim3 units((n + kRowsPerBlock - 1) / kRowsPerBlock, F);
   (void)hipMemsetAsync(png, 0, sizeof(EncPng) * F, st);
-  hipLaunchKernelGGL(k_png_scan, rows, dim3(kRowsPerBlock), 0, st, img, W, H, png, rowsum);
-  hipLaunchKernelGGL(k_png_codes, dim3(F), dim3(256), 0, st, png, rowsum, W, H);
-  hipLaunchKernelGGL(k_png_bits, rows, dim3(kRowsPerBlock), 0, st, img, W, H, png, rowbits);
-  hipLaunchKernelGGL(k_png_layout, dim3(F), dim3(256), 0, st, png, rowbits, H, fsize, nk, kslot);
+  hipLaunchKernelGGL(k_png_scan, units, dim3(kRowsPerBlock), 0, st, img, W, H, png, usum);
+  hipLaunchKernelGGL(k_png_codes, dim3(F), dim3(256), 0, st, png, usum, W, H);
+  hipLaunchKernelGGL(k_png_bits, units, dim3(kRowsPerBlock), 0, st, img, W, H, png, ubits);
+  hipLaunchKernelGGL(k_png_layout, dim3(F), dim3(256), 0, st, png, ubits, n, fsize, nk, kslot);
 }
 
-void launch_csv_sizes(const float* depth, uint32_t W, uint32_t H, uint32_t F, uint32_t* rowlen, uint64_t* fsize,
+void launch_csv_sizes(const float* depth, uint32_t W, uint32_t H, uint32_t F, uint32_t* ulen, uint64_t* fsize,
                       uint32_t nk, uint32_t kslot, hipStream_t st) {
-  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
-  hipLaunchKernelGGL(k_csv_len, rows, dim3(kRowsPerBlock), 0, st, depth, W, H, rowlen);
-  hipLaunchKernelGGL(k_csv_layout, dim3(F), dim3(256), 0, st, rowlen, H, fsize, nk, kslot);
+  const uint32_t n = csv_units_per_frame(W, H);
+  const dim3 units((n + kRowsPerBlock - 1) / kRowsPerBlock, F);
+  hipLaunchKernelGGL(k_csv_len, units, dim3(kRowsPerBlock), 0, st, depth, W, H, ulen);
+  hipLaunchKernelGGL(k_csv_layout, dim3(F), dim3(256), 0, st, ulen, n, fsize, nk, kslot);
 }
 
 void launch_file_layout(const uint64_t* fsize, uint32_t n_files, uint64_t* foff, const EncPng* png_a,
@@ -642,8 +712,9 @@ void launch_file_layout(const uint64_t* fsize, uint32_t n_files, uint64_t* foff,
 void launch_png_emit(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, const EncPng* png, const uint32_t* rowoff,
                      uint8_t* zbuf, const uint64_t* zbase, uint8_t* out, const uint64_t* foff, uint32_t nk,
                      uint32_t kslot, hipStream_t st) {
-  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
-  hipLaunchKernelGGL(k_png_emit, rows, dim3(kRowsPerBlock), 0, st, img, W, H, png, rowoff, zbuf, zbase);
+  const uint32_t n = png_units_per_frame(W, H);
+  hipLaunchKernelGGL(k_png_emit, dim3((n + kRowsPerBlock - 1) / kRowsPerBlock, F), dim3(kRowsPerBlock), 0, st, img, W,
+                     H, png, rowoff, zbuf, zbase);
   hipLaunchKernelGGL(k_png_ends, dim3(F), dim3(64), 0, st, png, zbuf, zbase);
   // chunks per frame: at most the worst-case stream size / 8 KiB
   const uint64_t max_z = (uint64_t)H * (3ull * W + 1ull) * 2ull + 65536ull;
@@ -662,8 +733,9 @@ void launch_depth_stats(const float* depth, uint32_t npx, uint32_t F, void* scra
 
 void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,
                      const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
-  const dim3 rows((H + kRowsPerBlock - 1) / kRowsPerBlock, F);
-  hipLaunchKernelGGL(k_csv_emit, rows, dim3(kRowsPerBlock), 0, st, depth, W, H, rowoff, out, foff, nk, kslot);
+  const uint32_t n = csv_units_per_frame(W, H);
+  hipLaunchKernelGGL(k_csv_emit, dim3((n + kRowsPerBlock - 1) / kRowsPerBlock, F), dim3(kRowsPerBlock), 0, st, depth,
+                     W, H, rowoff, out, foff, nk, kslot);
 }
 
 }  // namespace csg

@@ -142,7 +142,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     intr = wl.intr
     pose_cache = {}
     pending = []
-    t_render = 0.0
+    t_render = t_slot_wait = t_prep = t_main_wait = t_labels = 0.0
     t0 = time.time()
     starts = list(range(0, len(frames), batch))
 
@@ -151,7 +151,9 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         the label loop, in its own thread: the C-ABI call releases the GIL)."""
         fb = frames[starts[b]:starts[b] + batch]
         slot = b % pool.n_slots
+        tw = time.time()
         arrays = pool.arrays(slot)          # (waits until the writers are done with the slot)
+        tp = time.time()
         epochs = sorted({f // 10 for f in fb})
         set_of = {}
         for k, e in enumerate(epochs):
@@ -173,14 +175,20 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             arrays["file_offsets"] = offsets
         else:
             out = r.render(fr, want=want, out={k: v[:len(fb)] for k, v in arrays.items()})
-        return fb, slot, out, time.time() - tr
+        te = time.time()
+        return fb, slot, out, (te - tr, tp - tw, tr - tp)
 
     ahead = ThreadPoolExecutor(max_workers=1)
     try:
         nxt = ahead.submit(render_batch, 0) if starts else None
         for b in range(len(starts)):
-            fb, slot, out, dt = nxt.result()
+            tq = time.time()
+            fb, slot, out, (dt, dwait, dprep) = nxt.result()
+            t_main_wait += time.time() - tq
             t_render += dt
+            t_slot_wait += dwait
+            t_prep += dprep
+            tl = time.time()
             if b + 1 < len(starts):
                 nxt = ahead.submit(render_batch, b + 1)
             for e in sorted({f // 10 for f in fb}):
@@ -223,6 +231,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 fut = pool.submit(slot, k, files, lab, os.path.join(out_dir, "labels", f"label_{f:06d}.json"))
                 pending.append((fut, log_args))
             del out
+            t_labels += time.time() - tl
             # log frames in order as they complete
             while pending and pending[0][0].done():
                 _log_done(log, *pending.pop(0), "pointcloud" in outs)
@@ -236,6 +245,9 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     log.save()
     summary = log.summary()
     summary["throughput"] = {"frames": len(frames), "wall_s": round(wall, 3), "render_s": round(t_render, 3),
+                             "render_thread": {"render_s": round(t_render, 3), "slot_wait_s": round(t_slot_wait, 3),
+                                               "epoch_prep_s": round(t_prep, 3)},
+                             "main_thread": {"wait_render_s": round(t_main_wait, 3), "labels_s": round(t_labels, 3)},
                              "frames_per_s": round(len(frames) / wall, 2) if wall > 0 else None,
                              "writers": n_writers, "writer_mode": writer_mode, "outputs": sorted(outs)}
     return summary
