@@ -22,11 +22,11 @@ DEPS = SOURCES + [os.path.join(PKG, "csrc", "csg_kernels.h"), os.path.join(PKG, 
 ARCH = os.environ.get("CSG_OFFLOAD_ARCH", "gfx950")
 IO_LIB = os.path.join(PKG, "libcsgio.so")
 IO_SOURCES = [os.path.join(PKG, "csrc", "csg_io.cpp")]
-IO_DEPS = IO_SOURCES + [os.path.join(ROOT, "include", "csg_io.h")]
+IO_DEPS = IO_SOURCES + [os.path.join(ROOT, "include", "csg_io.h"), os.path.join(PKG, "csrc", "csg_repr.h")]
 IO_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread"]
 # _csgjson: the label-JSON encoder (CPython extension module)
 JSON_EXT = os.path.join(PKG, "_csgjson.so")
-JSON_SOURCES = [os.path.join(PKG, "csrc", "csg_json.cpp")]
+JSON_SOURCES = [os.path.join(PKG, "csrc", "csg_json.cpp"), os.path.join(PKG, "csrc", "csg_repr.h")]
 
 # -ffp-contract=off: the raster spec's float expressions must round exactly as
 # written (bit-exact with the CPU oracle).  HIP keeps fp32 '/' and sqrtf
@@ -75,7 +75,7 @@ def build_json(force: bool = False, verbose: bool = False) -> str:
         import sysconfig
         cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
         cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{sysconfig.get_paths()['include']}", "-o",
-               JSON_EXT + ".tmp", *JSON_SOURCES]
+               JSON_EXT + ".tmp", JSON_SOURCES[0]]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

@@ -29,7 +29,7 @@ constexpr int kClCodes = 19;          // code-length alphabet
 constexpr int kMaxBits = 15;          // deflate code length limit
 constexpr int kMaxClBits = 7;         // code-length code limit
 constexpr uint32_t kEob = 256;
-constexpr uint32_t kIdatBytes = 8192; // zlib bytes per IDAT chunk (one CRC per chunk)
+constexpr uint32_t kIdatBytes = 2048; // zlib bytes per IDAT chunk (one CRC, one GPU thread per chunk)
 constexpr uint32_t kMaxHeaderWords = 160;   // 2 zlib bytes + block header bits (< 4,800 bits)
 constexpr uint32_t kAdlerMod = 65521;
 
@@ -280,6 +280,38 @@ CSG_HD int put_dec_u64(char* out, uint64_t v) {
   return n;
 }
 
+CSG_HD int put_dec_u32(char* out, uint32_t v) {
+  char tmp[10];
+  int n = 0;
+  do {
+    tmp[n++] = (char)('0' + v % 10u);
+    v /= 10u;
+  } while (v);
+  for (int k = 0; k < n; ++k) out[k] = tmp[n - 1 - k];
+  return n;
+}
+
+CSG_HD int dec_digits_u32(uint32_t v) {
+  int n = 1;
+  while (v >= 10u) {
+    v /= 10u;
+    ++n;
+  }
+  return n;
+}
+
+// x * 10^6 rounded half to even, for x = m * 2^e (m < 2^24, e < 17).
+CSG_HD uint64_t scaled6(uint64_t m, int e) {
+  if (e >= 0) return (m << e) * 1000000u;   // m << e < 2^41: fits
+  const uint64_t n = m * 1000000u;          // < 2^44
+  const int sh = -e;
+  if (sh >= 64) return 0;
+  uint64_t q = n >> sh;
+  const uint64_t r = n & ((1ull << sh) - 1u), half = 1ull << (sh - 1);
+  if (r > half || (r == half && (q & 1u))) ++q;
+  return q;
+}
+
 CSG_HD int fmt6f(float x, char* out) {
   uint32_t u;
   __builtin_memcpy(&u, &x, 4);
@@ -332,19 +364,17 @@ CSG_HD int fmt6f(float x, char* out) {
     for (int d = 0; d < 6; ++d) out[p++] = '0';
     return p;
   }
-  uint64_t q;
-  if (e >= 0) {
-    q = (m << e) * 1000000u;   // m << e < 2^41: fits
-  } else {
-    const uint64_t n = m * 1000000u;   // < 2^44
-    const int sh = -e;
-    if (sh >= 64) {
-      q = 0;
-    } else {
-      q = n >> sh;
-      const uint64_t r = n & ((1ull << sh) - 1u), half = 1ull << (sh - 1);
-      if (r > half || (r == half && (q & 1u))) ++q;
+  const uint64_t q = scaled6(m, e);
+  if (q < (1ull << 32)) {   // |x| < ~4295 (depths): 32-bit digit arithmetic
+    const uint32_t q32 = (uint32_t)q, ip = q32 / 1000000u;
+    uint32_t f = q32 - ip * 1000000u;
+    p += put_dec_u32(out + p, ip);
+    out[p++] = '.';
+    for (int d = 5; d >= 0; --d) {
+      out[p + d] = (char)('0' + f % 10u);
+      f /= 10u;
     }
+    return p + 6;
   }
   const uint64_t ip = q / 1000000u;
   uint32_t f = (uint32_t)(q - ip * 1000000u);
@@ -355,6 +385,30 @@ CSG_HD int fmt6f(float x, char* out) {
     f /= 10u;
   }
   return p + 6;
+}
+
+// Length of fmt6f(x) without writing it.
+CSG_HD int fmt6f_len(float x) {
+  uint32_t u;
+  __builtin_memcpy(&u, &x, 4);
+  const uint32_t ex = (u >> 23) & 255u, mant = u & 0x7FFFFFu;
+  const int sign = (int)(u >> 31);
+  if (ex == 255u) return mant ? 3 : 3 + sign;
+  const uint64_t m = ex ? (mant | 0x800000u) : mant;
+  const int e = ex ? (int)ex - 150 : -149;
+  if (e >= 17) {
+    char tmp[kMaxF6Chars];
+    return fmt6f(x, tmp);
+  }
+  const uint64_t q = scaled6(m, e);
+  if (q < (1ull << 32)) return sign + dec_digits_u32((uint32_t)q / 1000000u) + 7;
+  uint64_t ip = q / 1000000u;
+  int n = 1;
+  while (ip >= 10u) {
+    ip /= 10u;
+    ++n;
+  }
+  return sign + n + 7;
 }
 
 }  // namespace dfl

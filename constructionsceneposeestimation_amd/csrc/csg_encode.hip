@@ -4,8 +4,8 @@
 // :1672-1673, :1690-1709) and the depth CSV (np.savetxt "%.6f" :1687-1688).
 // The host then only copies the packed bytes out and writes them.
 //
-// Work is parallel over segments of image rows (one thread per 512 bytes of a
-// PNG row stream, per 64 values of a CSV row):
+// Work is parallel over segments of image rows (one thread per 512 raw bytes
+// of a PNG row, per 64 values of a CSV row):
 //
 //   PNG, per image kind (csg_deflate.h for the formats):
 //     k_png_scan    Sub-filter the row on the fly, run-length tokens -> the
@@ -27,7 +27,7 @@
 //                   with plain stores, the two words it may share with its
 //                   neighbours with atomicOr (staging zeroed first)
 //   k_png_ends      zlib + block header, end-of-block code, Adler-32
-//   k_png_pack      one thread per 8-KiB IDAT chunk: copy into the file,
+//   k_png_pack      one thread per 2-KiB IDAT chunk: copy into the file,
 //                   chunk header, CRC-32 (LDS table); signature + IHDR and
 //                   IEND at the ends
 //   k_csv_emit      each row formats its values in place
@@ -50,55 +50,44 @@ namespace {
 constexpr int kRowsPerBlock = 64;   // one wave of units per workgroup (one frame per workgroup)
 // Work units: segments of rows, so that a batch offers tens of thousands of
 // threads (one thread per 1080p row left the GPU mostly idle).
-constexpr uint32_t kSegBytes = 512;  // PNG: filtered-stream bytes per unit
+constexpr uint32_t kSegBytes = 512;  // PNG: raw row bytes per unit
 constexpr uint32_t kSegVals = 64;    // CSV: values per unit
 
-__host__ __device__ __forceinline__ uint32_t png_units(uint32_t W) { return (3u * W + 1u + kSegBytes - 1u) / kSegBytes; }
+__host__ __device__ __forceinline__ uint32_t png_units(uint32_t W) { return (3u * W + kSegBytes - 1u) / kSegBytes; }
 __host__ __device__ __forceinline__ uint32_t csv_units(uint32_t W) { return (W + kSegVals - 1u) / kSegVals; }
 
-// Bytes [s0, s1) of the filtered PNG stream of an 8-bit RGB image row
-// (byte 0: filter type 1 = Sub; byte i > 0: raw[i - 1] - raw[i - 4], the
-// byte one pixel to the left, 0 before the row).  Units of kSegBytes of this
-// stream are tokenised independently: a run never crosses a unit boundary
-// (a literal starts each unit; valid deflate, a few bytes larger).
+// The filtered PNG stream of unit k of an 8-bit RGB image row: raw bytes
+// [k * kSegBytes, ...) each minus the byte one pixel (3 bytes) to its left (0
+// before the row: filter type 1, Sub), preceded in unit 0 by the filter-type
+// byte.  Units are tokenised independently: a run never crosses a unit
+// boundary (a literal starts each unit; valid deflate, a few bytes larger).
+// Rows with a 16-B aligned unit start stream 16-B loads, the next one issued
+// before the current one is tokenised.
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int t) {
+  const uint32_t w = t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w;
+  return (w >> (8 * (t & 3))) & 255u;
+}
+
 template <class Sink>
-__device__ __forceinline__ void png_seg_bytes(const uint8_t* row, uint32_t s0, uint32_t s1, Sink& sink) {
-  uint32_t i = s0;
-  if (i == 0) {
-    sink.push(1u);
-    ++i;
-  }
-  // raw bytes j = i - 1 .. s1 - 2, each minus raw[j - 3]; dword loads where aligned
-  const uintptr_t base = reinterpret_cast<uintptr_t>(row);
-  for (; i < s1 && ((base + i - 1) & 3u); ++i) {
-    const uint32_t j = i - 1;
-    sink.push((uint32_t)(row[j] - (j >= 3 ? row[j - 3] : 0)) & 255u);
-  }
-  uint32_t prev = 0;   // the dword before the current one (bytes j - 4 .. j - 1)
-  if (i < s1 && i - 1 >= 4) prev = *reinterpret_cast<const uint32_t*>(row + i - 5);
-  else if (i < s1) {
-    for (uint32_t k = 0; k < 4; ++k) {
-      const int j = (int)i - 5 + (int)k;
-      prev |= (j >= 0 ? (uint32_t)row[j] : 0u) << (8 * k);
-    }
-  }
-  for (; i + 4 <= s1; i += 4) {
-    const uint32_t cur = *reinterpret_cast<const uint32_t*>(row + i - 1);
-    // left neighbours (3 bytes back) of the 4 bytes of cur: bytes 1..3 of prev, byte 0 of cur
-    const uint32_t left = (prev >> 8) | (cur << 24);
-    const uint32_t jl = i - 1;   // raw index of cur's byte 0 (left valid from raw index 3)
+__device__ __forceinline__ void png_unit_bytes(const uint8_t* row, uint32_t W, uint32_t k, Sink& sink) {
+  const uint32_t j0 = k * kSegBytes, j1 = min(j0 + kSegBytes, 3u * W);
+  if (k == 0) sink.push(1u);
+  uint32_t j = j0;
+  if (((reinterpret_cast<uintptr_t>(row) + j0) & 15u) == 0 && j + 16u <= j1) {
+    uint4 prev = j0 ? *reinterpret_cast<const uint4*>(row + j0 - 16) : make_uint4(0u, 0u, 0u, 0u);
+    uint4 cur = *reinterpret_cast<const uint4*>(row + j);
+    for (; j + 16u <= j1; j += 16u) {
+      const uint4 nxt = j + 32u <= j1 ? *reinterpret_cast<const uint4*>(row + j + 16) : cur;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t b = (cur >> (8 * k)) & 255u;
-      const uint32_t l = jl + (uint32_t)k >= 3u ? (left >> (8 * k)) & 255u : 0u;
-      sink.push((b - l) & 255u);
+      for (int t = 0; t < 16; ++t) {
+        const uint32_t b = byte_of(cur, t), l = t >= 3 ? byte_of(cur, t - 3) : byte_of(prev, 13 + t);
+        sink.push((b - l) & 255u);
+      }
+      prev = cur;
+      cur = nxt;
     }
-    prev = cur;
   }
-  for (; i < s1; ++i) {
-    const uint32_t j = i - 1;
-    sink.push((uint32_t)(row[j] - (j >= 3 ? row[j - 3] : 0)) & 255u);
-  }
+  for (; j < j1; ++j) sink.push((uint32_t)(row[j] - (j >= 3u ? row[j - 3] : 0u)) & 255u);
 }
 
 // Adler sums of a byte stream starting from (0, 0), reduced lazily.
@@ -119,11 +108,13 @@ struct AdlerSums {
 // ---------------------------------------------------------------------------
 // PNG pass 1: histogram + Adler sums
 // ---------------------------------------------------------------------------
-// Unit u of a frame: row u / U, stream bytes [(u % U) * kSegBytes, ...).
-__device__ __forceinline__ void png_unit(uint32_t u, uint32_t W, uint32_t U, uint32_t& r, uint32_t& s0, uint32_t& s1) {
+// Unit u of a frame: row u / U, unit k = u % U of that row; its stream length.
+__device__ __forceinline__ void png_unit(uint32_t u, uint32_t U, uint32_t& r, uint32_t& k) {
   r = u / U;
-  s0 = (u - r * U) * kSegBytes;
-  s1 = min(s0 + kSegBytes, 3u * W + 1u);
+  k = u - r * U;
+}
+__device__ __forceinline__ uint32_t png_unit_len(uint32_t k, uint32_t W) {
+  return min((k + 1u) * kSegBytes, 3u * W) - k * kSegBytes + (k == 0 ? 1u : 0u);
 }
 
 __global__ __launch_bounds__(kRowsPerBlock) void k_png_scan(const uint8_t* __restrict__ img, uint32_t W, uint32_t H,
@@ -133,8 +124,8 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_scan(const uint8_t* __res
   for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) hist[s] = 0;
   __syncthreads();
   if (u < H * U) {
-    uint32_t r, s0, s1;
-    png_unit(u, W, U, r, s0, s1);
+    uint32_t r, k;
+    png_unit(u, U, r, k);
     AdlerSums ad;
     auto lit = [&](uint32_t b) { atomicAdd(&hist[b], 1u); };
     auto match = [&](uint32_t len) {
@@ -150,7 +141,7 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_scan(const uint8_t* __res
         tok.push(x);
       }
     } sink{{lit, match}, &ad};
-    png_seg_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, s0, s1, sink);
+    png_unit_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, k, sink);
     sink.tok.finish();
     usum[(size_t)f * H * U + u] = make_uint2((uint32_t)(ad.a % kAdlerMod), (uint32_t)(ad.b % kAdlerMod));
   }
@@ -249,7 +240,7 @@ __global__ __launch_bounds__(256) void k_png_codes(EncPng* __restrict__ png, con
   uint64_t l = 0;
   for (uint32_t u = lo; u < hi; ++u) {
     const uint2 v = rowsum[(size_t)f * n + u];
-    const uint32_t s0 = (u % U) * kSegBytes, len = min(s0 + kSegBytes, 3u * W + 1u) - s0;
+    const uint32_t len = png_unit_len(u % U, W);
     adler_cat(a, b, v.x, v.y, len);
     l += len;
   }
@@ -284,8 +275,8 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_bits(const uint8_t* __res
   for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) clen[s] = (uint8_t)(png[f].code[s] >> 16);
   __syncthreads();
   if (u >= H * U) return;
-  uint32_t r, s0, s1;
-  png_unit(u, W, U, r, s0, s1);
+  uint32_t r, k;
+  png_unit(u, U, r, k);
   uint32_t bits = 0;
   auto lit = [&](uint32_t b) { bits += clen[b]; };
   auto match = [&](uint32_t len) {
@@ -297,7 +288,7 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_bits(const uint8_t* __res
     RunTokenizer<decltype(lit)&, decltype(match)&> tok;
     __device__ void push(uint32_t x) { tok.push(x); }
   } sink{{lit, match}};
-  png_seg_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, s0, s1, sink);
+  png_unit_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, k, sink);
   sink.tok.finish();
   ubits[(size_t)f * H * U + u] = bits;
 }
@@ -357,8 +348,7 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_csv_len(const float* __restri
   const uint32_t r = u / V, x0 = (u - r * V) * kSegVals, x1 = min(x0 + kSegVals, W);
   const float* row = depth + ((size_t)f * H + r) * W;
   uint32_t n = x1 - x0;   // separators
-  char tmp[kMaxF6Chars];
-  for (uint32_t x = x0; x < x1; ++x) n += (uint32_t)fmt6f(row[x], tmp);
+  for (uint32_t x = x0; x < x1; ++x) n += (uint32_t)fmt6f_len(row[x]);
   ulen[(size_t)f * H * V + u] = n;
 }
 
@@ -437,8 +427,8 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_emit(const uint8_t* __res
   for (uint32_t s = threadIdx.x; s < (uint32_t)kLitCodes; s += kRowsPerBlock) code[s] = png[f].code[s];
   __syncthreads();
   if (u >= H * U) return;
-  uint32_t r, s0, s1;
-  png_unit(u, W, U, r, s0, s1);
+  uint32_t r, k;
+  png_unit(u, U, r, k);
   uint32_t* words = reinterpret_cast<uint32_t*>(zbuf + zbase[f]);
   WordBits wb;
   wb.init(words, png[f].hdr_bits + uoff[(size_t)f * H * U + u]);
@@ -454,7 +444,7 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_png_emit(const uint8_t* __res
     RunTokenizer<decltype(lit)&, decltype(match)&> tok;
     __device__ void push(uint32_t x) { tok.push(x); }
   } sink{{lit, match}};
-  png_seg_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, s0, s1, sink);
+  png_unit_bytes(img + ((size_t)f * H + r) * (size_t)W * 3u, W, k, sink);
   sink.tok.finish();
   wb.finish();
 }
@@ -716,7 +706,7 @@ void launch_png_emit(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, con
   hipLaunchKernelGGL(k_png_emit, dim3((n + kRowsPerBlock - 1) / kRowsPerBlock, F), dim3(kRowsPerBlock), 0, st, img, W,
                      H, png, rowoff, zbuf, zbase);
   hipLaunchKernelGGL(k_png_ends, dim3(F), dim3(64), 0, st, png, zbuf, zbase);
-  // chunks per frame: at most the worst-case stream size / 8 KiB
+  // chunks per frame: at most the worst-case stream size / kIdatBytes
   const uint64_t max_z = (uint64_t)H * (3ull * W + 1ull) * 2ull + 65536ull;
   const uint32_t max_ch = (uint32_t)((max_z + kIdatBytes - 1) / kIdatBytes);
   hipLaunchKernelGGL(k_png_pack, dim3((max_ch + 63) / 64, F), dim3(64), 0, st, png, zbuf, zbase, out, foff, W, H, nk,

@@ -4,6 +4,8 @@
 // GIL) while the GPU renders the next batch.
 #include "../../include/csg_io.h"
 
+#include "csg_repr.h"
+
 #include <zlib.h>
 
 #include <cerrno>
@@ -277,6 +279,88 @@ int csgio_write_pointcloud_txt(const char* path, const float* xyz, const uint8_t
     used = (size_t)(p - buf.data());
   }
   if (used && !f.write(buf.data(), used)) return -EIO;
+  return f.close();
+}
+
+int csgio_write_label_json(const char* path, const csgio_label* L) {
+  if (!path || !L || !L->camera_pose || !L->camera_params || !L->class_mapping || (L->n_objects && (!L->obj_head ||
+      !L->obj_label || !L->obj_kp_off)) || (L->n_labels && !L->inst_stats) || (L->n_kp && (!L->kp_uv || !L->kp_vis ||
+      !L->kp_name)))
+    return -EINVAL;
+  std::string o;
+  o.reserve(131072);
+  char num[48];
+  auto put_int = [&](long long v) { o.append(num, std::to_chars(num, num + sizeof num, v).ptr); };
+  auto put_dbl = [&](double v) {
+    if (std::isnan(v)) o += "NaN";
+    else if (std::isinf(v)) o += v > 0 ? "Infinity" : "-Infinity";
+    else o.append(num, csg::repr_double(num, v));
+  };
+  o += "{\n  \"frame_id\": ";
+  put_int(L->frame_id);
+  o += ",\n  \"camera_pose\": [";
+  for (int k = 0; k < 7; ++k) {
+    o += k ? ",\n    " : "\n    ";
+    put_dbl(L->camera_pose[k]);
+  }
+  o += "\n  ],\n  \"camera_params\": ";
+  o += L->camera_params;
+  o += ",\n  \"objects\": ";
+  uint32_t n_vis = 0;
+  for (uint32_t j = 0; j < L->n_objects; ++j) {
+    const int32_t lab = L->obj_label[j];
+    if (lab < 0 || (uint32_t)lab >= L->n_labels) continue;
+    const uint32_t* st = L->inst_stats + (size_t)lab * 5;
+    if (st[0] == 0) continue;
+    o += n_vis++ ? ",\n    {\n" : "[\n    {\n";
+    o += L->obj_head[j];
+    o += ",\n      \"pixel_count\": ";
+    put_int(st[0]);
+    o += ",\n      \"bbox_2d\": [";
+    for (int k = 1; k < 5; ++k) {
+      o += k > 1 ? ",\n        " : "\n        ";
+      put_int(st[k]);
+    }
+    o += "\n      ]";
+    if (L->covered) {   // occlusionRatio: 1 - visible / covered, float32 (labels.occlusion_ratios); -1 unknown
+      const uint32_t cv = L->covered[lab];
+      const uint32_t cnt = cv & 0x7FFFFFFFu;
+      const float occ = (!(cv & 0x80000000u) && cnt) ? (float)(1.0 - (double)st[0] / (double)cnt) : -1.0f;
+      o += ",\n      \"occlusion_ratio\": ";
+      put_dbl((double)occ);
+    }
+    const uint32_t k0 = L->obj_kp_off[j], k1 = L->obj_kp_off[j + 1];
+    if (k1 > k0) {
+      o += ",\n      \"keypoints_2d\": [";
+      for (uint32_t q = k0; q < k1; ++q) {
+        const uint32_t k = L->obj_kp[q];
+        o += q > k0 ? ",\n        [\n          " : "\n        [\n          ";
+        o += L->kp_name[k];
+        o += ",\n          ";
+        put_dbl((double)L->kp_uv[2 * k]);
+        o += ",\n          ";
+        put_dbl((double)L->kp_uv[2 * k + 1]);
+        o += ",\n          ";
+        put_int(L->kp_vis[k]);
+        o += "\n        ]";
+      }
+      o += "\n      ]";
+    }
+    o += "\n    }";
+  }
+  o += n_vis ? "\n  ]" : "[]";
+  o += ",\n  \"instance_mask_shape\": [\n    ";
+  put_int(L->height);
+  o += ",\n    ";
+  put_int(L->width);
+  o += "\n  ],\n  \"num_objects\": ";
+  put_int(n_vis);
+  o += ",\n  \"class_mapping\": ";
+  o += L->class_mapping;
+  o += "\n}";
+  File f(path);
+  if (!f.f) return -errno;
+  if (!f.write(o.data(), o.size())) return -EIO;
   return f.close();
 }
 

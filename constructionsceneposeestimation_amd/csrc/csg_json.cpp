@@ -22,6 +22,8 @@
 
 #include <charconv>
 
+#include "csg_repr.h"
+
 typedef struct {
   char* p;
   Py_ssize_t n, cap;
@@ -102,55 +104,10 @@ static int put_obj_str(Buf* b, PyObject* s) {   /* a str object's text as-is */
   return put(b, u, n);
 }
 
-/* repr(float) of a finite double */
+/* repr(float) of a finite double (csg_repr.h) */
 static int put_repr_double(Buf* b, double x) {
-  char sci[40];
-  const auto r = std::to_chars(sci, sci + sizeof sci, x, std::chars_format::scientific);
-  const char* p = sci;
-  const char* end = r.ptr;
   if (grow(b, 48)) return -1;
-  char* o = b->p + b->n;
-  if (*p == '-') {
-    *o++ = '-';
-    ++p;
-  }
-  char dig[24] = {0};
-  int nd = 0;
-  while (p < end && *p != 'e') {
-    if (*p != '.') dig[nd++] = *p;
-    ++p;
-  }
-  int e10 = 0;                   /* "e+XX" / "e-XX" (not NUL-terminated) */
-  std::from_chars(p + 1 + (p[1] == '+'), end, e10);
-  const int decpt = e10 + 1;     /* value = 0.d1d2... x 10^decpt */
-  if (decpt <= -4 || decpt > 16) {
-    *o++ = dig[0];
-    if (nd > 1) {
-      *o++ = '.';
-      for (int k = 1; k < nd; ++k) *o++ = dig[k];
-    }
-    *o++ = 'e';
-    int ex = decpt - 1;
-    *o++ = ex < 0 ? '-' : '+';
-    if (ex < 0) ex = -ex;
-    if (ex < 10) *o++ = '0';
-    o = std::to_chars(o, o + 4, ex).ptr;
-  } else if (decpt <= 0) {
-    *o++ = '0';
-    *o++ = '.';
-    for (int k = 0; k < -decpt; ++k) *o++ = '0';
-    for (int k = 0; k < nd; ++k) *o++ = dig[k];
-  } else if (decpt >= nd) {
-    for (int k = 0; k < nd; ++k) *o++ = dig[k];
-    for (int k = nd; k < decpt; ++k) *o++ = '0';
-    *o++ = '.';
-    *o++ = '0';
-  } else {
-    for (int k = 0; k < decpt; ++k) *o++ = dig[k];
-    *o++ = '.';
-    for (int k = decpt; k < nd; ++k) *o++ = dig[k];
-  }
-  b->n = o - b->p;
+  b->n = csg::repr_double(b->p + b->n, x) - b->p;
   return 0;
 }
 

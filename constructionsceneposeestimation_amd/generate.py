@@ -37,6 +37,7 @@ import os
 import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
+from functools import partial
 from typing import List, Optional
 
 import numpy as np
@@ -48,6 +49,7 @@ from .renderer import Renderer, make_frames, output_spec, scene_labels
 from .shard import shard_of_range
 from .workload import Workload
 from .writer_pool import WriterPool
+from .writers import LabelWriter
 from .writer_pool import _write_png  # noqa: F401  (the generator's PNG settings; tools/gen_bench.py)
 
 
@@ -140,6 +142,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         pool.use_pinned(r.host_buffer, batch * sum(est[k] for k in kinds) + (1 << 20) if kinds else 0)
     nk = len(kinds)
     intr = wl.intr
+    # thread mode: label files written natively from the frame's arrays (no GIL)
+    lw = LabelWriter(wl.kp_table, wl.intr.params(), scene_labels(wl.scene), wl.height, wl.width) if gpu_files else None
     pose_cache = {}
     pending = []
     t_render = t_slot_wait = t_prep = t_main_wait = t_labels = 0.0
@@ -196,10 +200,18 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                     pose_cache[e] = object_poses(wl.scene, wl.epoch(e).object_frames)
             for k, f in enumerate(fb):
                 V, P, C, cam, aim, q = wl.camera(f)
-                lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
-                                   out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
-                                   wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k])
-                log_args = dict(n_objects=lab["num_objects"], kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
+                if lw is not None:
+                    ep = lw.epoch(f // 10, pose_cache[f // 10])
+                    lab = partial(lw.write, frame_id=f, camera_pose=cm.get_obj_pose_from_matrix(C), ep=ep,
+                                  inst_stats=out["inst_stats"][k], covered=out["label_covered"][k],
+                                  kp_uv=out["keypoints_uv"][k], kp_vis=out["keypoints_vis"][k])
+                    n_obj = lw.n_visible(ep, out["inst_stats"][k])
+                else:
+                    lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
+                                       out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
+                                       wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k])
+                    n_obj = lab["num_objects"]
+                log_args = dict(n_objects=n_obj, kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
                                 cam_pos=cam, depth_range=out["depth_range"][k].copy() if "depth_range" in out else None)
                 if "depth_stats" in out:   # valid, zero, inf, sum, min, max (csg_outputs.depth_stats)
                     v = out["depth_stats"][k].tolist()

@@ -64,8 +64,10 @@ def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, st
     """Every file of frame ``k`` of a batch, then its label JSON (the resume
     marker, GDP:1357-1367 scans labels/).  ``files`` = (path, kind, array
     names); kind "encoded" names the file index j in the batch's files
-    encoded on the GPU (arrays "files" + "file_offsets"); returns the frame's
-    depth counts for the quality log."""
+    encoded on the GPU (arrays "files" + "file_offsets"); ``label`` is the
+    label dict, or a callable that writes the label file to the path it is
+    given (writers.LabelWriter); returns the frame's depth counts for the
+    quality log."""
     from . import writers as fileio
     from .labels import label_json_bytes
     for path, kind, keys in files:
@@ -85,7 +87,10 @@ def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, st
             _atomic(path, fileio.write_pointcloud_txt, *a)
         else:
             raise ValueError(kind)
-    _atomic(label_path, _write_bytes, label_json_bytes(label))
+    if callable(label):   # a native label writer job (writers.LabelWriter.write bound to the frame)
+        _atomic(label_path, label)
+    else:
+        _atomic(label_path, _write_bytes, label_json_bytes(label))
     return fileio.depth_stats(arrays["depth"][k]) if "depth" in arrays else None
 
 

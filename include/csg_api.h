@@ -155,7 +155,7 @@ typedef struct {
 /* csg_outputs.file_kinds */
 #define CSG_FILE_RGB_PNG 1u        /* 8-bit RGB PNG of the frame (cv2.imwrite, GDP:1672-1673): filter Sub,
                                       one dynamic-Huffman deflate block of literals and distance-1 matches,
-                                      8 KiB IDAT chunks */
+                                      2 KiB IDAT chunks */
 #define CSG_FILE_DEPTH_CSV 2u      /* np.savetxt(depth, fmt="%.6f", delimiter=" ") text (GDP:1687-1688),
                                       byte-identical */
 #define CSG_FILE_DEPTH_PNG 4u      /* the JET depth visualisation (csg_outputs.depth_vis) as a PNG

@@ -190,6 +190,7 @@ static int csv(uint32_t W, uint32_t H, const char* in, const char* outp) {
   for (uint32_t r = 0; r < H; ++r)
     for (uint32_t x = 0; x < W; ++x) {
       const int n = fmt6f(v[(size_t)r * W + x], buf);
+      if (fmt6f_len(v[(size_t)r * W + x]) != n) return 4;   // the length-only form must agree
       fwrite(buf, 1, (size_t)n, fo);
       fputc(x + 1 < W ? ' ' : '\n', fo);
     }

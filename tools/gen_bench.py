@@ -115,7 +115,8 @@ def main():
         print(json.dumps({
             "frames": a.frames, "seconds": round(dt, 3), "frames_per_s": s["throughput"]["frames_per_s"],
             "frames_per_s_incl_setup": round(a.frames / dt, 1),
-            "render_s": s["throughput"]["render_s"], "writers": a.writers, "writer_mode": a.writer_mode, "bytes_written": size,
+            "render_s": s["throughput"]["render_s"], "render_thread": s["throughput"]["render_thread"],
+            "main_thread": s["throughput"]["main_thread"], "wall_s": s["throughput"]["wall_s"], "writers": a.writers, "writer_mode": a.writer_mode, "bytes_written": size,
             "bytes_per_frame": round(size / a.frames), "workload": a.workload,
             "outputs": list(outputs) + ["label.json"], "successful": s["counters"]["successful_frames"],
             "encode_ms_per_frame": ms, "encode_bytes_per_frame": sizes, "encode_ms_sum": round(enc, 2),
