@@ -91,7 +91,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
              resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
-             writer_mode: str = "thread") -> dict:
+             writer_mode: str = "thread", renderers: int = 0) -> dict:
     """Render ``frames`` on one GPU and write them (``outputs``, default the
     reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
     add the depth .npy, the depth .npy + CSV, the point cloud, the normals).
@@ -132,10 +132,15 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
                 + (["normals"] if "normals" in outs else []))
     n_writers = writers or default_writers()
+    # Renderer contexts on the device, each with its own stream and work
+    # buffers, rendering alternate batches from their own threads: one batch's
+    # encode and device-to-host copy overlaps the next one's render.
+    n_rend = renderers or (2 if gpu_files else 1)
     # the writer processes start here, before this process touches the GPU
     pool = WriterPool(output_spec(batch, wl.height, wl.width, wl.n_keypoints(), scene_labels(wl.scene), want),
-                      n_writers, n_slots=3, mode=writer_mode)
-    r = Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device)
+                      n_writers, n_slots=2 + n_rend, mode=writer_mode)
+    rends = [Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device) for _ in range(n_rend)]
+    r = rends[0]
     if gpu_files:   # page-locked slots, and buffers for the encoded files (an estimate, grown on demand)
         npx = wl.width * wl.height
         est = {"rgb_png": 2 * npx, "depth_csv": 10 * npx, "depth_png": npx}
@@ -155,6 +160,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         the label loop, in its own thread: the C-ABI call releases the GIL)."""
         fb = frames[starts[b]:starts[b] + batch]
         slot = b % pool.n_slots
+        r = rends[b % n_rend]
         tw = time.time()
         arrays = pool.arrays(slot)          # (waits until the writers are done with the slot)
         tp = time.time()
@@ -182,19 +188,19 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         te = time.time()
         return fb, slot, out, (te - tr, tp - tw, tr - tp)
 
-    ahead = ThreadPoolExecutor(max_workers=1)
+    ahead = ThreadPoolExecutor(max_workers=n_rend)
     try:
-        nxt = ahead.submit(render_batch, 0) if starts else None
+        queued = [ahead.submit(render_batch, b) for b in range(min(n_rend, len(starts)))]
         for b in range(len(starts)):
             tq = time.time()
-            fb, slot, out, (dt, dwait, dprep) = nxt.result()
+            fb, slot, out, (dt, dwait, dprep) = queued.pop(0).result()
             t_main_wait += time.time() - tq
             t_render += dt
             t_slot_wait += dwait
             t_prep += dprep
             tl = time.time()
-            if b + 1 < len(starts):
-                nxt = ahead.submit(render_batch, b + 1)
+            if b + n_rend < len(starts):   # (renderer b % n_rend is free again)
+                queued.append(ahead.submit(render_batch, b + n_rend))
             for e in sorted({f // 10 for f in fb}):
                 if e not in pose_cache:
                     pose_cache[e] = object_poses(wl.scene, wl.epoch(e).object_frames)
@@ -252,7 +258,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     finally:
         ahead.shutdown(wait=True)
         pool.close()
-        r.close()
+        for x in rends:
+            x.close()
     wall = time.time() - t0
     log.save()
     summary = log.summary()
@@ -261,7 +268,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                                                "epoch_prep_s": round(t_prep, 3)},
                              "main_thread": {"wait_render_s": round(t_main_wait, 3), "labels_s": round(t_labels, 3)},
                              "frames_per_s": round(len(frames) / wall, 2) if wall > 0 else None,
-                             "writers": n_writers, "writer_mode": writer_mode, "outputs": sorted(outs)}
+                             "writers": n_writers, "writer_mode": writer_mode, "renderers": n_rend,
+                             "outputs": sorted(outs)}
     return summary
 
 
@@ -285,13 +293,15 @@ def main(argv=None):
     ap.add_argument("--normals", action="store_true")
     ap.add_argument("--writers", type=int, default=0, help="writer processes (0: the CPUs this process may use)")
     ap.add_argument("--writer-mode", default="thread", choices=("thread", "process"))
+    ap.add_argument("--renderers", type=int, default=0,
+                    help="renderer contexts rendering alternate batches (0: 2 with writer threads, else 1)")
     ap.add_argument("--no-resume", action="store_true")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
                        a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
-                       outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode)
+                       outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode, renderers=a.renderers)
     print(json.dumps(summary))
 
 

@@ -95,16 +95,17 @@ def main():
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--outputs", default="reference")
     ap.add_argument("--writer-mode", default="thread", choices=("thread", "process"))
+    ap.add_argument("--renderers", type=int, default=0)
     a = ap.parse_args()
     outputs = parse_outputs(a.outputs)
     out = tempfile.mkdtemp(prefix="csg_gen_")
     try:
         generate(out, list(range(a.batch)), a.workload, seed=9, batch=a.batch, writers=a.writers,
-                 outputs=outputs, writer_mode=a.writer_mode)   # warm-up
+                 outputs=outputs, writer_mode=a.writer_mode, renderers=a.renderers)   # warm-up
         shutil.rmtree(out)
         t0 = time.perf_counter()
         s = generate(out, list(range(a.frames)), a.workload, seed=0, batch=a.batch, writers=a.writers,
-                     outputs=outputs, writer_mode=a.writer_mode)
+                     outputs=outputs, writer_mode=a.writer_mode, renderers=a.renderers)
         dt = time.perf_counter() - t0
         size = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(out) for f in fs)
         shutil.rmtree(out)
@@ -116,7 +117,8 @@ def main():
             "frames": a.frames, "seconds": round(dt, 3), "frames_per_s": s["throughput"]["frames_per_s"],
             "frames_per_s_incl_setup": round(a.frames / dt, 1),
             "render_s": s["throughput"]["render_s"], "render_thread": s["throughput"]["render_thread"],
-            "main_thread": s["throughput"]["main_thread"], "wall_s": s["throughput"]["wall_s"], "writers": a.writers, "writer_mode": a.writer_mode, "bytes_written": size,
+            "main_thread": s["throughput"]["main_thread"], "wall_s": s["throughput"]["wall_s"], "writers": a.writers, "writer_mode": a.writer_mode,
+            "renderers": s["throughput"]["renderers"], "bytes_written": size,
             "bytes_per_frame": round(size / a.frames), "workload": a.workload,
             "outputs": list(outputs) + ["label.json"], "successful": s["counters"]["successful_frames"],
             "encode_ms_per_frame": ms, "encode_bytes_per_frame": sizes, "encode_ms_sum": round(enc, 2),
