@@ -156,10 +156,24 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     t0 = time.time()
     starts = list(range(0, len(frames), batch))
 
+    def prepare(b: int):
+        """Host state of batch b (epoch layouts, object poses, cameras), made
+        ahead in its own thread so the render thread only renders."""
+        fb = frames[starts[b]:starts[b] + batch]
+        for e in sorted({f // 10 for f in fb}):
+            st = wl.epoch(e)
+            if e not in pose_cache:
+                if len(pose_cache) >= 256:   # bounded over long runs (an epoch is met once)
+                    pose_cache.pop(next(iter(pose_cache)))
+                pose_cache[e] = object_poses(wl.scene, st.object_frames)
+        wl.frame_params(fb)
+
     def render_batch(b: int):
         """Batch b into its slot of the writer ring (runs one batch ahead of
         the label loop, in its own thread: the C-ABI call releases the GIL)."""
         fb = frames[starts[b]:starts[b] + batch]
+        if b < len(prep_f):
+            prep_f[b].result()
         slot = b % pool.n_slots
         r = rends[b % n_rend]
         tw = time.time()
@@ -190,7 +204,16 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         return fb, slot, out, (te - tr, tp - tw, tr - tp)
 
     ahead = ThreadPoolExecutor(max_workers=n_rend)
+    prep = ThreadPoolExecutor(max_workers=1)
+    prep_f: List = []
+    kPrepAhead = 3
+
+    def prep_until(b: int) -> None:
+        while len(prep_f) < min(b, len(starts)):
+            prep_f.append(prep.submit(prepare, len(prep_f)))
+
     try:
+        prep_until(kPrepAhead + n_rend)
         queued = [ahead.submit(render_batch, b) for b in range(min(n_rend, len(starts)))]
         for b in range(len(starts)):
             tq = time.time()
@@ -200,6 +223,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             t_slot_wait += dwait
             t_prep += dprep
             tl = time.time()
+            prep_until(b + n_rend + kPrepAhead + 1)
             if b + n_rend < len(starts):   # (renderer b % n_rend is free again)
                 queued.append(ahead.submit(render_batch, b + n_rend))
             for e in sorted({f // 10 for f in fb}):
@@ -258,6 +282,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             _log_done(log, *p, "pointcloud" in outs)
     finally:
         ahead.shutdown(wait=True)
+        prep.shutdown(wait=True)
         pool.close()
         for x in rends:
             x.close()
