@@ -96,9 +96,10 @@ def main():
     ap.add_argument("--outputs", default="reference")
     ap.add_argument("--writer-mode", default="thread", choices=("thread", "process"))
     ap.add_argument("--renderers", type=int, default=0)
+    ap.add_argument("--dir", default=None, help="file system to write to (default $TMPDIR; /dev/shm: RAM)")
     a = ap.parse_args()
     outputs = parse_outputs(a.outputs)
-    out = tempfile.mkdtemp(prefix="csg_gen_")
+    out = tempfile.mkdtemp(prefix="csg_gen_", dir=a.dir)
     try:
         generate(out, list(range(a.batch)), a.workload, seed=9, batch=a.batch, writers=a.writers,
                  outputs=outputs, writer_mode=a.writer_mode, renderers=a.renderers)   # warm-up
@@ -118,7 +119,7 @@ def main():
             "frames_per_s_incl_setup": round(a.frames / dt, 1),
             "render_s": s["throughput"]["render_s"], "render_thread": s["throughput"]["render_thread"],
             "main_thread": s["throughput"]["main_thread"], "wall_s": s["throughput"]["wall_s"], "writers": a.writers, "writer_mode": a.writer_mode,
-            "renderers": s["throughput"]["renderers"], "bytes_written": size,
+            "renderers": s["throughput"]["renderers"], "dir": os.path.dirname(out), "bytes_written": size,
             "bytes_per_frame": round(size / a.frames), "workload": a.workload,
             "outputs": list(outputs) + ["label.json"], "successful": s["counters"]["successful_frames"],
             "encode_ms_per_frame": ms, "encode_bytes_per_frame": sizes, "encode_ms_sum": round(enc, 2),
