@@ -87,7 +87,7 @@ def parse_outputs(spec: str) -> tuple:
     return out
 
 
-def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 60,
+def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 30,
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
              resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
@@ -305,7 +305,7 @@ def main(argv=None):
     ap.add_argument("--frames", type=int, default=41, help="total frames of the run (all shards)")
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--batch", type=int, default=60)
+    ap.add_argument("--batch", type=int, default=30)
     ap.add_argument("--rank", type=int, default=int(os.environ.get("RANK", "0")))
     ap.add_argument("--world", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--device", type=int, default=int(os.environ.get("LOCAL_RANK", "0")))
