@@ -122,3 +122,13 @@ def test_generate_gpu_files_match_host_writers(tmp_path):
                 assert a == b, name
             n += 1
     assert n == 9 * 5
+
+
+def test_files_c5_4k():
+    """One C5 frame at 3840x2160 (22.5 PNG units and 60 CSV units per row,
+    ~25 MB of raw RGB per image)."""
+    from constructionsceneposeestimation_amd.workload import Workload
+    wl = Workload("C5", seed=0)
+    assert (wl.width, wl.height) == (3840, 2160)
+    out, blobs = _render(wl, [1205])
+    _check(out, blobs, 1)
