@@ -963,15 +963,25 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 #ifndef CSG_WAVES
 #define CSG_WAVES 6             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
 #endif
+#ifndef CSG_COV_STAGE
+#define CSG_COV_STAGE 88        // k_raster<true>: smaller batches pay for the coverage table (6 workgroups per CU)
+#endif
+#ifndef CSG_COV_WAVES
+#define CSG_COV_WAVES 6
+#endif
 #if CSG_WAVES > 0
-#define CSG_RASTER_ATTR __attribute__((amdgpu_waves_per_eu(kCov ? 5 : CSG_WAVES, kCov ? 5 : CSG_WAVES)))
+#define CSG_RASTER_ATTR \
+  __attribute__((amdgpu_waves_per_eu(kCov ? CSG_COV_WAVES : CSG_WAVES, kCov ? CSG_COV_WAVES : CSG_WAVES)))
 #else
 #define CSG_RASTER_ATTR
 #endif
 constexpr int kStage = CSG_STAGE;     // records staged per raster batch (<= kBlock)
-static_assert(kStage <= kBlock, "one staged record per thread");
+static_assert(kStage <= kBlock && CSG_COV_STAGE <= kBlock, "one staged record per thread");
+template <bool kCov>
+constexpr int kStageOf = kCov ? CSG_COV_STAGE : kStage;
+template <int NS>
 struct RecImage {
-  uint4 q[kRecGroups][kStage];
+  uint4 q[kRecGroups][NS];
 };
 
 // Coverage table of k_raster<true> (occlusion, GDP:1780-1790 occlusionRatio):
@@ -981,7 +991,6 @@ struct RecImage {
 // one tile) marks the tile: its labels are then flagged unknown and their
 // counts are not added, so the result does not depend on fragment order.
 struct CovLds {
-  int32_t rlabel[kStage];               // label of each staged record (-1: not counted)
   uint32_t keys[kCovSlots];             // label of each slot (kNoAlpha: empty)
   uint32_t mask[kCovSlots][kTile];      // per slot: bit lx of word ly
   uint32_t ovf;                         // some label found no slot
@@ -996,6 +1005,7 @@ struct RasterCtx {
   uint32_t dbg;
   uint32_t* ctr;   // profiling counters (CSG_DEBUG 512 only)
   CovLds* cov;     // k_raster<true> only
+  int32_t* rlabel; // k_raster<true> only: label of each staged record (-1: not counted)
   uint32_t* gcov;  // covered[f][.] of this frame (k_raster<true> only)
 };
 
@@ -1017,6 +1027,23 @@ __device__ __forceinline__ void cov_mark(const RasterCtx& c, uint32_t label, int
   atomicOr(&c.gcov[label], kCovUnknown);
 }
 
+// Slot of `label` in the coverage table, or -1 if it has none yet (read-only
+// probe).  Slots are never freed and fill in probe order, so an empty slot
+// ends the search; a slot taken concurrently reads as "none", which only
+// sends the fragment to cov_mark.
+__device__ __forceinline__ int cov_find(const RasterCtx& c, uint32_t label) {
+  const CovLds& t = *c.cov;
+  const uint32_t h = label & (uint32_t)(kCovSlots - 1);
+#pragma clang loop vectorize(disable) unroll(disable)
+  for (uint32_t p = 0; p < (uint32_t)kCovSlots; ++p) {
+    const uint32_t idx = (h + p) & (uint32_t)(kCovSlots - 1);
+    const uint32_t cur = t.keys[idx];
+    if (cur == label) return (int)idx;
+    if (cur == kNoAlpha) return -1;
+  }
+  return -1;
+}
+
 
 __device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
 
@@ -1025,8 +1052,8 @@ __device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
 // alpha test (texture described inline in the record), then ds_min_u64.
 // With kCov (occlusion) every fragment in the depth range is alpha-tested,
 // early-z or not, and a surviving one marks its label's coverage bit.
-template <bool kCov>
-__device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, int k, int lx, int ly) {
+template <bool kCov, int NS>
+__device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>& I, int k, int lx, int ly) {
   const int px = c.ox + lx, py = c.oy + ly;
   const uint4 g2 = I.q[2][k], g3 = I.q[3][k], g4 = I.q[4][k];
   const float A[3] = {f_(g2.z), f_(g2.w), f_(g3.x)}, B[3] = {f_(g3.y), f_(g3.z), f_(g3.w)};
@@ -1037,6 +1064,19 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
   if constexpr (kCov) {
+    // A fragment has two possible effects: its label's coverage bit and the
+    // depth minimum.  One that loses early-z and whose bit is already set has
+    // neither, so it skips the alpha test (both are monotone: a stale read only
+    // sends a fragment down the full path).
+    const int32_t lab = c.rlabel[k];
+    const bool zwin = key < *z;
+    int slot = -1;
+    bool mark = false;
+    if (lab >= 0) {
+      slot = cov_find(c, (uint32_t)lab);
+      mark = slot < 0 || !((c.cov->mask[slot][ly] >> lx) & 1u);
+    }
+    if (!zwin && !mark) return;
     if (g2.y != kNoAlpha) {
       const uint4 g5 = I.q[5][k], g6 = I.q[6][k];
       const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
@@ -1044,9 +1084,11 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
       interp_uv(e, ssum, uv, u, v);
       if (!alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)g6.w, u, v)) return;
     }
-    const int32_t lab = c.cov->rlabel[k];
-    if (lab >= 0) cov_mark(c, (uint32_t)lab, lx, ly);
-    atomicMin(z, key);
+    if (mark) {
+      if (slot >= 0) atomicOr(&c.cov->mask[slot][ly], 1u << lx);
+      else cov_mark(c, (uint32_t)lab, lx, ly);
+    }
+    if (zwin) atomicMin(z, key);
     return;
   }
 #if CSG_OPAQUE_DIRECT
@@ -1074,11 +1116,12 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage& I, 
 }
 
 // Stage bin entry `idx` into `slot`; returns its row count inside the tile.
+template <int NS>
 __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t* bins, uint32_t idx, uint32_t end,
-                                                 uint32_t rec_cap, RecImage& img, int slot, int ox, int oy,
+                                                 uint32_t rec_cap, RecImage<NS>& img, int slot, int ox, int oy,
                                                  uint32_t& row0) {
   row0 = 0;
-  const uint32_t r = (idx < end && slot < kStage) ? bins[idx] : 0xFFFFFFFFu;
+  const uint32_t r = (idx < end && slot < NS) ? bins[idx] : 0xFFFFFFFFu;
   if (r >= rec_cap) return 0;
   const uint4* src = reinterpret_cast<const uint4*>(recs + r);
   uint4 q[kRecGroups];
@@ -1141,12 +1184,13 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
   return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
 
+template <int NS>
 struct RasterLds {
-  RecImage img;                         // staged bin records
+  RecImage<NS> img;                     // staged bin records
 #if CSG_L1_BITMAP
-  uint32_t starts1[kStage];             // bit i: a staged record's rows start at level-1 item i
-  uint16_t before1[kStage + 1];         // records starting before item 32*d
-  uint32_t crec[kStage];                // compact record: slot | first item << 8
+  uint32_t starts1[NS];                 // bit i: a staged record's rows start at level-1 item i
+  uint16_t before1[NS + 1];             // records starting before item 32*d
+  uint32_t crec[NS];                    // compact record: slot | first item << 8
 #else
   uint32_t pre[kBlock + 1];             // row-item prefix per record
 #endif
@@ -1167,22 +1211,22 @@ struct RasterLds {
 // An item finds its record / span by a rank query over a bitmap of starts
 // (measured: -5.5% k_raster vs a 4-ary search over the prefix; a per-item
 // owner map cost a workgroup per CU in LDS).
-template <bool kCov>
-__device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev& s, const BatchDev& b, RasterLds& L,
+template <bool kCov, int NS>
+__device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev& s, const BatchDev& b, RasterLds<NS>& L,
                                              uint32_t beg, uint32_t end, const uint32_t* bins, const Rec* recs) {
   const int tid = threadIdx.x;
-  for (uint32_t base = beg; base < end; base += kStage) {
+  for (uint32_t base = beg; base < end; base += NS) {
     uint32_t row0;
     const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
     L.row0[tid] = (uint8_t)row0;
     if constexpr (kCov) {   // label of the staged record (read back from this thread's own slot)
-      if (tid < kStage) {
+      if (tid < NS) {
         int32_t lab = -1;
         if (rows) {
           lab = s.inst[L.img.q[2][tid].x >> kUidShift].label;
           if (lab >= 0 && (uint32_t)lab >= b.n_labels) lab = -1;
         }
-        c.cov->rlabel[tid] = lab;
+        c.rlabel[tid] = lab;
       }
     }
     if ((DBG(b.dbg) & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
@@ -1197,7 +1241,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
 #if CSG_L1_BITMAP
     // records with rows get compact indices; item -> record is a rank query
     // over a bitmap of record starts (as for level 2 below)
-    if (tid < kStage) L.starts1[tid] = 0u;   // ordered before the atomics by the scan's barriers
+    if (tid < NS) L.starts1[tid] = 0u;   // ordered before the atomics by the scan's barriers
     if (tid == 0) L.before1[0] = 0;
     uint32_t tot1p;
     const uint32_t ex1p = block_excl_scan(rows | (rows ? 0x10000u : 0u), L.wsum, tot1p);
@@ -1448,9 +1492,28 @@ struct ResolveLds {
 // The resolve's LDS aliases the raster loop's in a union inside k_raster.
 // (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4;
 // 26,656 B keeps 6.)
-static_assert((sizeof(RasterLds) > sizeof(ResolveLds) ? sizeof(RasterLds) : sizeof(ResolveLds)) + kTilePix * 8 <=
-                  (CSG_WAVES >= 7 ? 22528u : CSG_WAVES == 6 ? 26700u : CSG_WAVES == 5 ? 32256u : 40960u),
+constexpr size_t lds_budget(int waves) {
+  return waves >= 7 ? 22528u : waves == 6 ? 26700u : waves == 5 ? 32256u : 40960u;
+}
+static_assert((sizeof(RasterLds<kStage>) > sizeof(ResolveLds) ? sizeof(RasterLds<kStage>) : sizeof(ResolveLds)) +
+                      kTilePix * 8 <= lds_budget(CSG_WAVES),
               "k_raster LDS must allow CSG_WAVES workgroups per CU");
+
+// The raster loop's side of the union; k_raster<true> adds the coverage table
+// (it is flushed before the resolve starts, so the resolve may reuse it).
+template <bool kCov>
+struct RasterSide {
+  RasterLds<kStageOf<kCov>> r;
+};
+template <>
+struct RasterSide<true> {
+  RasterLds<kStageOf<true>> r;
+  CovLds cov;
+  int32_t rlabel[kStageOf<true>];       // label of each staged record (-1: not counted)
+};
+static_assert((sizeof(RasterSide<true>) > sizeof(ResolveLds) ? sizeof(RasterSide<true>) : sizeof(ResolveLds)) +
+                      kTilePix * 8 <= lds_budget(CSG_COV_WAVES),
+              "k_raster<true> LDS must allow CSG_COV_WAVES workgroups per CU");
 
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
 __device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
@@ -1542,18 +1605,19 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
 }
 
 // kCov: also the per-label coverage for occlusion (b.covered); a separate
-// instantiation (4.7 KiB more LDS: 5 workgroups per CU), launched only when
-// the caller asks for it.
+// instantiation launched only when the caller asks for it.  Its coverage table
+// (4.1 KiB) is paid for with smaller batches (CSG_COV_STAGE records), so it
+// keeps 6 workgroups per CU.
 template <bool kCov>
 __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, BatchDev b) {
   __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
-  __shared__ CovLds covl;                            // kCov only (unreferenced otherwise: not allocated)
+  constexpr int NS = kStageOf<kCov>;
 #ifdef CSG_LDS_PAD
   __shared__ volatile uint32_t ldspad[CSG_LDS_PAD / 4];   // A/B only: occupancy probe
   if (b.dbg == 0xDEADu) ldspad[threadIdx.x] = 1u;
 #endif
   __shared__ union Lds {
-    RasterLds r;                                     // raster loop
+    RasterSide<kCov> ra;                             // raster loop
     ResolveLds q;                                    // resolve
   } L;
   const int tid = threadIdx.x;
@@ -1575,21 +1639,27 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     return;
   }
   for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
+  CovLds* covp = nullptr;
+  int32_t* rlabel = nullptr;
   if constexpr (kCov) {
+    covp = &L.ra.cov;
+    rlabel = L.ra.rlabel;
+    CovLds& covl = *covp;
     for (int p = tid; p < kCovSlots * kTile; p += kBlock) (&covl.mask[0][0])[p] = 0u;
     if (tid < kCovSlots) covl.keys[tid] = kNoAlpha;
     if (tid == 0) covl.ovf = 0u;
   }
   const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
   const Rec* recs = b.recs + (size_t)f * b.rec_cap;
-  RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow, &covl,
+  RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow, covp, rlabel,
               kCov ? b.covered + (size_t)f * b.n_labels : nullptr};
   __syncthreads();
-  raster_block<kCov>(c, s, b, L.r, beg, end, bins, recs);
+  raster_block<kCov, NS>(c, s, b, L.ra.r, beg, end, bins, recs);
   __syncthreads();
   if constexpr (kCov) {
     // per slot: popcount of its 32 mask words, 8 threads per slot (4 words
     // each, lanes t..t+7 of one wave); the table is read-only from here on
+    const CovLds& covl = *covp;
     static_assert(kCovSlots * 8 == kBlock && kTile == 32, "8 threads x 4 words per slot");
     const uint32_t sl = (uint32_t)tid >> 3, w0 = ((uint32_t)tid & 7u) * 4u;
     uint32_t n = 0;
@@ -1603,6 +1673,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       if (covl.ovf) atomicOr(&c.gcov[lab], kCovUnknown);
       else atomicAdd(&c.gcov[lab], n);
     }
+    __syncthreads();   // the resolve reuses the table's LDS
   }
 
   if (DBG(b.dbg) & 1u) {   // ablation: keep the raster loop alive, skip the resolve
