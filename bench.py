@@ -47,7 +47,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "annotated frames/sec (RGB+seg+2D kpts) at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-RECORD_BYTES = 112 + 4  # k_setup writes one 112-B raster record + its 4-B tile rectangle per record
+RECORD_BYTES = 96 + 4  # k_setup writes one 96-B raster record + its 4-B tile rectangle per record
 DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 240
 
 
@@ -142,7 +142,7 @@ def roofline(b_geom: int, b_tex: int, b_out: int, frames_per_launch: float, rast
              "B_out + B_tex: outputs written once, bound textures read once"),
         kern("k_setup", round(b_geom + frames_per_launch * records_per_frame * RECORD_BYTES), setup_ms,
              "B_geom once per launch (the launch's frames share the geometry through L2 and the Infinity "
-             "Cache: the grid runs frame-fast) + 116 B written per raster record (k_clip + k_setup)"),
+             "Cache: the grid runs frame-fast) + 100 B written per raster record (k_clip + k_setup)"),
     ]
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic.get("k_raster"), "kernel": "k_raster",

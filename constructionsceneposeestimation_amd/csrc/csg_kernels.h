@@ -36,20 +36,23 @@ struct Chunk {                    // <= 256 triangles of one instance + their ob
 static_assert(sizeof(Chunk) == 48, "Chunk layout");
 
 // One raster (sub-)triangle: fixed-point screen vertices for coverage plus the
-// homogeneous coefficients of its ORIGINAL triangle for depth/attributes.
+// screen-space planes of its ORIGINAL triangle (spec §3.5-6): 1/W and, for
+// alpha-tested materials, u/W and v/W.  Field groups of 16 B as k_setup
+// writes and k_raster stages them: 0 x0 x1 x2 y0 | 1 y1 y2 p0 p1 |
+// 2 uid atex D0 D1 | 3 D2 U0 U1 U2 | 4 V0 V1 V2 atex_wh | 5 athr.
 struct __attribute__((aligned(16))) Rec {
   int32_t x[3], y[3];          // 24: 24.8 fixed point, positive orientation
   uint16_t px0, py0, px1, py1; // 8 : inclusive pixel bbox, clamped to the frame
   uint32_t uid;                // 4
   uint32_t atex;               // 4 : alpha-test texture, texel offset (kNoAlpha: none)
-  float A[3], B[3], C[3];      // 36: e_k = A_k*x + B_k*y + C_k
-  float invdet;                // 4
-  float uv[6];                 // 24: only read for alpha-tested materials
+  float D[3];                  // 12: 1/W = (D0*x + D1*y) + D2 at pixel centre (x, y)
+  float U[3], V[3];            // 24: u/W, v/W planes (alpha-tested materials; zeros otherwise)
   uint32_t atex_wh;            // 4 : alpha texture width | height << 16
   uint32_t athr;               // 4 : alpha threshold (keep iff alpha > athr)
+  uint32_t pad[3];             // 12
 };
-static_assert(sizeof(Rec) == 112, "Rec layout");
-constexpr int kRecGroups = 7;  // 16-B field groups k_raster stages (the 112 B of payload)
+static_assert(sizeof(Rec) == 96, "Rec layout");
+constexpr int kRecGroups = 6;  // 16-B field groups (the 96 B of the record)
 
 struct FrameDev {                // csg_frame mirror
   float view[16];

@@ -58,9 +58,6 @@ namespace csg {
 #ifndef CSG_ALPHA_CLASS
 #define CSG_ALPHA_CLASS 1      // alpha tests decided by the 2-bit quad class where it can (see alpha_pass)
 #endif
-#ifndef CSG_SETUP_TRANSPOSE
-#define CSG_SETUP_TRANSPOSE 1  // k_setup stores each wave's records as consecutive 16-B chunks via LDS
-#endif
 #ifndef CSG_SMALL_COVER
 #define CSG_SMALL_COVER 4      // records with at most N x N pixel centres get an exact cover test in k_setup (0: off)
 #endif
@@ -106,20 +103,30 @@ __device__ __forceinline__ void hom_setup(const Cv3* v, Hom& h) {
   h.invdet = h.ok ? 1.0f / det : 0.0f;
 }
 
-__device__ __forceinline__ void hom_eval(const float* A, const float* B, const float* C, float invdet, int px, int py,
-                                         float* e, float& ssum, float& invw) {
-  const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) e[k] = (A[k] * fx + B[k] * fy) + C[k];
-  ssum = (e[0] + e[1]) + e[2];
-  invw = ssum * invdet;
+// Screen-space planes of the original triangle (spec §3.5-6), from its
+// homogeneous edge rows: with e_k = A_k*x + B_k*y + C_k, 1/W = invdet * sum e_k
+// and u/W = invdet * sum e_k u_k are affine in (x, y):
+//   D = (((A0 + A1) + A2) * invdet, (B...) * invdet, (C...) * invdet)
+//   U = (((A0*u0 + A1*u1) + A2*u2) * invdet, ...), V likewise with v.
+// uv = u0 v0 u1 v1 u2 v2.
+__device__ __forceinline__ void depth_plane(const float* A, const float* B, const float* C, float invdet, float* D) {
+  D[0] = ((A[0] + A[1]) + A[2]) * invdet;
+  D[1] = ((B[0] + B[1]) + B[2]) * invdet;
+  D[2] = ((C[0] + C[1]) + C[2]) * invdet;
+}
+__device__ __forceinline__ void uv_planes(const float* A, const float* B, const float* C, float invdet,
+                                          const float* uv, float* U, float* V) {
+  U[0] = ((A[0] * uv[0] + A[1] * uv[2]) + A[2] * uv[4]) * invdet;
+  U[1] = ((B[0] * uv[0] + B[1] * uv[2]) + B[2] * uv[4]) * invdet;
+  U[2] = ((C[0] * uv[0] + C[1] * uv[2]) + C[2] * uv[4]) * invdet;
+  V[0] = ((A[0] * uv[1] + A[1] * uv[3]) + A[2] * uv[5]) * invdet;
+  V[1] = ((B[0] * uv[1] + B[1] * uv[3]) + B[2] * uv[5]) * invdet;
+  V[2] = ((C[0] * uv[1] + C[1] * uv[3]) + C[2] * uv[5]) * invdet;
 }
 
-__device__ __forceinline__ void interp_uv(const float* e, float ssum, const float* uv, float& u, float& v) {
-  const float rs = 1.0f / ssum;
-  const float l0 = e[0] * rs, l1 = e[1] * rs, l2 = e[2] * rs;
-  u = (l0 * uv[0] + l1 * uv[2]) + l2 * uv[4];
-  v = (l0 * uv[1] + l1 * uv[3]) + l2 * uv[5];
+// A plane at pixel centre (fx, fy) = (px + 0.5, py + 0.5).
+__device__ __forceinline__ float plane_at(float p0, float p1, float p2, float fx, float fy) {
+  return (p0 * fx + p1 * fy) + p2;
 }
 
 // Bilinear RGBA8, repeat wrap, 8-bit fixed weights (v flipped: row 0 = top).
@@ -350,7 +357,11 @@ __global__ __launch_bounds__(256) void k_clip(SceneDev s, BatchDev b) {
 // k_setup
 // ---------------------------------------------------------------------------
 // Build one raster record from screen-space vertices; false if it covers no pixel.
-__device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, const float* sv, Rec& r) {
+// Groups 0-1 of a raster record (x0 x1 x2 y0 | y1 y2 p0 p1): the part that
+// differs between the sub-triangles of one clipped triangle.
+struct SubRec { uint4 g0, g1; };
+
+__device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, const float* sv, SubRec& r) {
   int32_t x[3], y[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -413,22 +424,15 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
     py0 += __ffs(rows) - 1;
   }
 #endif
-#pragma unroll
-  for (int k = 0; k < 3; ++k) { r.x[k] = x[k]; r.y[k] = y[k]; }
-  r.px0 = (uint16_t)px0; r.py0 = (uint16_t)py0; r.px1 = (uint16_t)px1; r.py1 = (uint16_t)py1;
+  r.g0 = make_uint4((uint32_t)x[0], (uint32_t)x[1], (uint32_t)x[2], (uint32_t)y[0]);
+  r.g1 = make_uint4((uint32_t)y[1], (uint32_t)y[2], (uint32_t)px0 | ((uint32_t)py0 << 16),
+                    (uint32_t)px1 | ((uint32_t)py1 << 16));
   return true;
 }
 
-__device__ __forceinline__ uint32_t rec_tile_rect(const Rec& r) {
-  return (uint32_t)(r.px0 / kTile) | ((uint32_t)(r.py0 / kTile) << 8) | ((uint32_t)(r.px1 / kTile) << 16) |
-         ((uint32_t)(r.py1 / kTile) << 24);
-}
-
-__device__ __forceinline__ void store_rec(Rec* dst, const Rec& r) {
-  const uint4* src = reinterpret_cast<const uint4*>(&r);
-  uint4* d = reinterpret_cast<uint4*>(dst);
-#pragma unroll
-  for (int k = 0; k < kRecGroups; ++k) d[k] = src[k];
+__device__ __forceinline__ uint32_t rec_tile_rect(const SubRec& r) {
+  const uint32_t px0 = r.g1.z & 0xFFFFu, py0 = r.g1.z >> 16, px1 = r.g1.w & 0xFFFFu, py1 = r.g1.w >> 16;
+  return (px0 / kTile) | ((py0 / kTile) << 8) | ((px1 / kTile) << 16) | ((py1 / kTile) << 24);
 }
 
 __device__ __forceinline__ uint32_t rect_area(uint32_t rc) {
@@ -491,7 +495,11 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     if (cull || (DBG(b.dbg) & 64u)) return;   // identical in every wave of the block (64: ablation, cull all)
   }
 
-  Rec r0, r1;   // named, never runtime-indexed (a Rec[2] would live in scratch)
+  // Records: groups 0-1 per sub-triangle (r0, r1: named, never runtime-
+  // indexed, which would put them in scratch), groups 2-5 shared (the
+  // original triangle's uid, alpha texture and planes).
+  SubRec r0, r1;
+  uint4 c2 = make_uint4(0u, 0u, 0u, 0u), c3 = c2, c4 = c2, c5 = c2;
   int nrec = 0;
   if ((uint32_t)tid < ch.count) {
     const uint32_t t = ch.start + tid;
@@ -562,7 +570,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
         su[0] = a.x * ra; sv[0] = a.y * ra;
         su[1] = bb.x * rb; sv[1] = bb.y * rb;
         su[2] = cc.x * rc; sv[2] = cc.y * rc;
-        Rec rr;
+        SubRec rr;
         if (make_rec(s, su, sv, rr)) {
           if (nrec == 0) r0 = rr; else r1 = rr;
           ++nrec;
@@ -581,12 +589,6 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
           nrec = 0;
         } else {
           const MatDesc mat = b.mats[(size_t)b.fset[f] * b.n_mat + m.material];
-          float uv[6] = {0, 0, 0, 0, 0, 0};
-          if (mat.alpha_test && m.has_uv) {
-            const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) uv[k] = tu[k];
-          }
           uint32_t atex = kNoAlpha, atex_wh = 0, athr = 0;
           if (mat.alpha_test && mat.texture >= 0) {
             const TexDesc td = s.texd[mat.texture];
@@ -594,19 +596,19 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
             atex_wh = td.width | (td.height << 16);
             athr = mat.alpha_threshold;
           }
-          auto fill = [&](Rec& rr) {
-            rr.uid = uid;
-            rr.atex = atex;
-            rr.atex_wh = atex_wh;
-            rr.athr = athr;
+          float D[3], U[3] = {0.0f, 0.0f, 0.0f}, V[3] = {0.0f, 0.0f, 0.0f};
+          depth_plane(h.A, h.B, h.C, h.invdet, D);
+          if (mat.alpha_test && m.has_uv) {   // uvs loaded only now: few values live at once
+            const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
+            float uv[6];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) { rr.A[k] = h.A[k]; rr.B[k] = h.B[k]; rr.C[k] = h.C[k]; }
-            rr.invdet = h.invdet;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) rr.uv[k] = uv[k];
-          };
-          fill(r0);
-          if (nrec > 1) fill(r1);
+            for (int k = 0; k < 6; ++k) uv[k] = tu[k];
+            uv_planes(h.A, h.B, h.C, h.invdet, uv, U, V);
+          }
+          c2 = make_uint4(uid, atex, __float_as_uint(D[0]), __float_as_uint(D[1]));
+          c3 = make_uint4(__float_as_uint(D[2]), __float_as_uint(U[0]), __float_as_uint(U[1]), __float_as_uint(U[2]));
+          c4 = make_uint4(__float_as_uint(V[0]), __float_as_uint(V[1]), __float_as_uint(V[2]), atex_wh);
+          c5 = make_uint4(athr, 0u, 0u, 0u);
         }
       }
     }
@@ -620,33 +622,33 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   if (lane == 0 && wtot) wbase = atomicAdd(&b.rec_count[f * kCounterStride], wtot);
   wbase = __shfl(wbase, 0, 64);
   if (DBG(b.dbg) & 128u) {   // ablation: no record stores
-    if (nrec == 3 && b.inst) b.inst[0] = r0.uid + r1.uid;
+    if (nrec == 3 && b.inst) b.inst[0] = r0.g0.x + r1.g0.x + c2.x + c3.x + c4.x + c5.x;
     return;
   }
-#if CSG_SETUP_TRANSPOSE
   // Coalesced record stores.  The wave's records take the contiguous slots
-  // [wbase, wbase + wtot), but lane-by-lane 16-B stores at a 112-B stride
-  // write ~7x more partial 128-B lines than the bytes need.  So, 16 records
+  // [wbase, wbase + wtot), but lane-by-lane 16-B stores at a 96-B stride
+  // write many more partial 128-B lines than the bytes need.  So, 16 records
   // at a time, the lanes holding them put them in a per-wave LDS stage and the
   // wave stores the stage as consecutive 16-B chunks (1 KB per instruction).
   // Wave-local: the loop count is uniform per wave, so there is no block barrier.
+  static_assert(16 * kRecGroups <= 2 * 64, "two chunk stores per lane");
   __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
   uint4* sw = tstage[tid >> 6];
   if (lane == 0 && wbase + wtot > b.rec_cap) atomicOr(b.overflow, 1u);
   uint4* dst = reinterpret_cast<uint4*>(b.recs + (size_t)f * b.rec_cap);
   const size_t lim = (size_t)b.rec_cap * kRecGroups;
-  uint4 q0[kRecGroups], q1[kRecGroups];
-  __builtin_memcpy(q0, &r0, sizeof(Rec));
-  __builtin_memcpy(q1, &r1, sizeof(Rec));
+  auto put = [&](uint32_t at, const SubRec& r) {
+    uint4* o = sw + at * kRecGroups;
+    o[0] = r.g0;
+    o[1] = r.g1;
+    o[2] = c2;
+    o[3] = c3;
+    o[4] = c4;
+    o[5] = c5;
+  };
   for (uint32_t p0 = 0; p0 < wtot; p0 += 16) {
-    if (nrec > 0 && mine - p0 < 16u) {
-#pragma unroll
-      for (int k = 0; k < kRecGroups; ++k) sw[(mine - p0) * kRecGroups + k] = q0[k];
-    }
-    if (nrec > 1 && mine + 1u - p0 < 16u) {
-#pragma unroll
-      for (int k = 0; k < kRecGroups; ++k) sw[(mine + 1u - p0) * kRecGroups + k] = q1[k];
-    }
+    if (nrec > 0 && mine - p0 < 16u) put(mine - p0, r0);
+    if (nrec > 1 && mine + 1u - p0 < 16u) put(mine + 1u - p0, r1);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const uint32_t nch = min(16u, wtot - p0) * kRecGroups;
@@ -659,18 +661,6 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   }
   if (nrec > 0 && wbase + mine < b.rec_cap) b.rect[(size_t)f * b.rec_cap + wbase + mine] = rec_tile_rect(r0);
   if (nrec > 1 && wbase + mine + 1 < b.rec_cap) b.rect[(size_t)f * b.rec_cap + wbase + mine + 1] = rec_tile_rect(r1);
-#else
-  auto emit = [&](const Rec& rec, uint32_t slot) {
-    if (slot >= b.rec_cap) {
-      atomicOr(b.overflow, 1u);
-      return;
-    }
-    store_rec(b.recs + (size_t)f * b.rec_cap + slot, rec);
-    b.rect[(size_t)f * b.rec_cap + slot] = rec_tile_rect(rec);
-  };
-  if (nrec > 0) emit(r0, wbase + mine);
-  if (nrec > 1) emit(r1, wbase + mine + 1);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -932,12 +922,10 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // ---------------------------------------------------------------------------
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
-// LDS image of up to kStage staged records as seven 16-B field groups (the Rec
-// layout cut at 16-B boundaries), group-major: lanes reading one group of
-// different records hit consecutive 16-B slots (no bank conflicts; a Rec-
-// strided image puts 8 records on each set of banks), lanes reading the same
-// record broadcast.  Groups: 0 x0 x1 x2 y0 | 1 y1 y2 p0 p1 | 2 uid atex A0 A1 |
-// 3 A2 B0 B1 B2 | 4 C0 C1 C2 invdet | 5 uv0-3 | 6 uv4 uv5 atex_wh athr.
+// LDS image of up to kStage staged records as their six 16-B field groups (see
+// Rec), group-major: lanes reading one group of different records hit
+// consecutive 16-B slots (no bank conflicts; a record-strided image puts 8
+// records on each set of banks), lanes reading the same record broadcast.
 //
 // Occupancy: k_raster is latency-bound (LDS and VMEM dependency chains), and
 // waves per SIMD are its lever (measured on C3 against 4 waves: 3 waves +22%
@@ -1054,13 +1042,18 @@ __device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
 // early-z or not, and a surviving one marks its label's coverage bit.
 template <bool kCov, int NS>
 __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>& I, int k, int lx, int ly) {
-  const int px = c.ox + lx, py = c.oy + ly;
-  const uint4 g2 = I.q[2][k], g3 = I.q[3][k], g4 = I.q[4][k];
-  const float A[3] = {f_(g2.z), f_(g2.w), f_(g3.x)}, B[3] = {f_(g3.y), f_(g3.z), f_(g3.w)};
-  const float C[3] = {f_(g4.x), f_(g4.y), f_(g4.z)};
-  float e[3], ssum, invw;
-  hom_eval(A, B, C, f_(g4.w), px, py, e, ssum, invw);
+  const float fx = (float)(c.ox + lx) + 0.5f, fy = (float)(c.oy + ly) + 0.5f;
+  const uint4 g2 = I.q[2][k], g3 = I.q[3][k];
+  const float invw = plane_at(f_(g2.z), f_(g2.w), f_(g3.x), fx, fy);
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
+  // alpha test at the pixel centre: u = U(x, y) * (1 / (1/W)), v likewise
+  auto alpha_ok = [&]() {
+    const uint4 g4 = I.q[4][k], g5 = I.q[5][k];
+    const float r = 1.0f / invw;
+    const float u = plane_at(f_(g3.y), f_(g3.z), f_(g3.w), fx, fy) * r;
+    const float v = plane_at(f_(g4.x), f_(g4.y), f_(g4.z), fx, fy) * r;
+    return alpha_pass(c.aquad, c.acls, g2.y, g4.w, (int)g5.x, u, v);
+  };
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
   if constexpr (kCov) {
@@ -1077,13 +1070,7 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
       mark = slot < 0 || !((c.cov->mask[slot][ly] >> lx) & 1u);
     }
     if (!zwin && !mark) return;
-    if (g2.y != kNoAlpha) {
-      const uint4 g5 = I.q[5][k], g6 = I.q[6][k];
-      const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
-      float u, v;
-      interp_uv(e, ssum, uv, u, v);
-      if (!alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)g6.w, u, v)) return;
-    }
+    if (g2.y != kNoAlpha && !alpha_ok()) return;
     if (mark) {
       if (slot >= 0) atomicOr(&c.cov->mask[slot][ly], 1u << lx);
       else cov_mark(c, (uint32_t)lab, lx, ly);
@@ -1104,11 +1091,7 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
     return;
   }
   if (!(DBG(c.dbg) & 4u) && g2.y != kNoAlpha) {
-    const uint4 g5 = I.q[5][k], g6 = I.q[6][k];
-    const float uv[6] = {f_(g5.x), f_(g5.y), f_(g5.z), f_(g5.w), f_(g6.x), f_(g6.y)};
-    float u, v;
-    interp_uv(e, ssum, uv, u, v);
-    const bool pass = alpha_pass(c.aquad, c.acls, g2.y, g6.z, (int)g6.w, u, v);
+    const bool pass = alpha_ok();
     if (DBG(c.dbg) & 512u) atomicAdd(&c.ctr[pass ? 6 : 5], 1u);   // profiling: alpha tests passed / failed
     if (!pass) return;
   }
@@ -1343,10 +1326,12 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
 // ---------------------------------------------------------------------------
 // per-pixel resolve
 // ---------------------------------------------------------------------------
-// Everything the resolve needs about one winning triangle (84 B).
+// Everything the resolve needs about one winning triangle (84 B).  P holds the
+// homogeneous edge rows A0-2 B0-2 C0-2, invdet and the uvs while the entry is
+// set up, then the screen planes D0-2 U0-2 V0-2 of 1/W, u/W, v/W (spec
+// §3.5-6; U, V for textured triangles only).
 struct ShadeEntry {
-  float A[3], B[3], C[3], invdet;   // homogeneous edge coefficients of the original triangle
-  float uv[6];
+  float P[16];
   int32_t label;
   int32_t tex;                      // -1: flat albedo
   uint32_t base;                    // albedo multiplier r | g << 8 | b << 16
@@ -1376,7 +1361,7 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   e.base = (uint32_t)mat.base[0] | ((uint32_t)mat.base[1] << 8) | ((uint32_t)mat.base[2] << 16);
   const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
 #pragma unroll
-  for (int z = 0; z < 6; ++z) e.uv[z] = tex >= 0 ? tu[z] : 0.0f;
+  for (int z = 0; z < 6; ++z) e.P[10 + z] = tex >= 0 ? tu[z] : 0.0f;
   // Homogeneous coefficients: for texture coordinates, depth / points and the
   // normals' facing sign only (a flat-shaded triangle without those outputs
   // needs none of them: no clip transform, no IEEE reciprocal).
@@ -1393,8 +1378,8 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
     Hom h;
     hom_setup(v, h);
 #pragma unroll
-    for (int z = 0; z < 3; ++z) { e.A[z] = h.A[z]; e.B[z] = h.B[z]; e.C[z] = h.C[z]; }
-    e.invdet = h.invdet;
+    for (int z = 0; z < 3; ++z) { e.P[z] = h.A[z]; e.P[3 + z] = h.B[z]; e.P[6 + z] = h.C[z]; }
+    e.P[9] = h.invdet;
     facing = h.invdet < 0.0f;
   }
   // world-space edges e1 = pw1 - pw0, e2 = pw2 - pw0, one model row (= one
@@ -1441,6 +1426,17 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   }
   e.q01 = q[0] | (q[1] << 16);
   e.q2 = q[2];
+  // The planes, from the entry's LDS copy: a separate phase, so the edge rows
+  // and uvs are not all live in registers together with the setup's state.
+  __asm__ volatile("" ::: "memory");
+  float P[16];
+#pragma unroll
+  for (int z = 0; z < 16; ++z) P[z] = e.P[z];
+  float D[3], U[3], V[3];
+  depth_plane(P, P + 3, P + 6, P[9], D);
+  uv_planes(P, P + 3, P + 6, P[9], P + 10, U, V);
+#pragma unroll
+  for (int z = 0; z < 3; ++z) { e.P[z] = D[z]; e.P[3 + z] = U[z]; e.P[6 + z] = V[z]; }
 }
 
 // Depth, instance id and RGB of pixel (px, py) covered by entry e.
@@ -1449,16 +1445,17 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
 __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry& e, int px, int py, bool need_depth,
                                             uint32_t& rgb_out, int32_t& id_out, float& depth_out) {
   const bool textured = e.tex >= 0 && !(DBG(s.dbg) & 4096u);   // 4096: ablation only, no texture fetch
-  float ev[3], ssum = 0.0f, invw = 0.0f;
-  if (need_depth || textured) hom_eval(e.A, e.B, e.C, e.invdet, px, py, ev, ssum, invw);
-  depth_out = need_depth ? 1.0f / invw : INFINITY;
+  const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+  float r = INFINITY;
+  if (need_depth || textured) r = 1.0f / plane_at(e.P[0], e.P[1], e.P[2], fx, fy);
+  depth_out = need_depth ? r : INFINITY;
   id_out = e.label;
   int base[3] = {(int)(e.base & 255u), (int)((e.base >> 8) & 255u), (int)((e.base >> 16) & 255u)};
   int alb[3];
   if (textured) {
-    float u, v;
+    const float u = plane_at(e.P[3], e.P[4], e.P[5], fx, fy) * r;
+    const float v = plane_at(e.P[6], e.P[7], e.P[8], fx, fy) * r;
     int c[4];
-    interp_uv(ev, ssum, e.uv, u, v);
     tex_sample(s, e.tex, u, v, c);
 #pragma unroll
     for (int z = 0; z < 3; ++z) alb[z] = div255(__umul24((uint32_t)c[z], (uint32_t)base[z]) + 127u);
@@ -1771,7 +1768,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
         ShadeEntry& e = L.q.tab[tid];
         if (DBG(b.dbg) & 8192u) {   // ablation only: no triangle setup (garbage shading)
           e = ShadeEntry{};
-          e.invdet = 1.0f; e.tex = -1; e.label = 0;
+          e.P[2] = 1.0f; e.tex = -1; e.label = 0;
         } else {
           shade_setup(s, b, f, u, e);
         }

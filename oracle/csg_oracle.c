@@ -50,6 +50,7 @@ typedef struct {
   float A[3], B[3], C[3];
   float invdet;
   int ok;
+  float D[3], U[3], V[3];   /* 1/W, u/W, v/W screen planes (hom_planes) */
 } hom_t;
 
 static void hom_setup(const cv3* v, hom_t* h) {
@@ -65,12 +66,27 @@ static void hom_setup(const cv3* v, hom_t* h) {
   h->invdet = h->ok ? 1.0f / det : 0.0f;
 }
 
-/* e_k at the pixel centre, s = sum, invW = s * invdet. */
-static inline void hom_eval(const hom_t* h, int px, int py, float* e, float* s, float* invw) {
-  const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
-  for (int k = 0; k < 3; ++k) e[k] = (h->A[k] * fx + h->B[k] * fy) + h->C[k];
-  *s = (e[0] + e[1]) + e[2];
-  *invw = *s * h->invdet;
+/* Spec 5-6: the screen planes of 1/W, u/W and v/W.  With e_k = A_k x + B_k y
+ * + C_k, 1/W = invdet * sum e_k and u/W = invdet * sum e_k u_k are affine:
+ * D = (((A0 + A1) + A2) * invdet, ...), U = (((A0 u0 + A1 u1) + A2 u2) * invdet,
+ * ...), V likewise with v. */
+static void hom_planes(hom_t* h, const float uv[3][2]) {
+  h->D[0] = ((h->A[0] + h->A[1]) + h->A[2]) * h->invdet;
+  h->D[1] = ((h->B[0] + h->B[1]) + h->B[2]) * h->invdet;
+  h->D[2] = ((h->C[0] + h->C[1]) + h->C[2]) * h->invdet;
+  h->U[0] = ((h->A[0] * uv[0][0] + h->A[1] * uv[1][0]) + h->A[2] * uv[2][0]) * h->invdet;
+  h->U[1] = ((h->B[0] * uv[0][0] + h->B[1] * uv[1][0]) + h->B[2] * uv[2][0]) * h->invdet;
+  h->U[2] = ((h->C[0] * uv[0][0] + h->C[1] * uv[1][0]) + h->C[2] * uv[2][0]) * h->invdet;
+  h->V[0] = ((h->A[0] * uv[0][1] + h->A[1] * uv[1][1]) + h->A[2] * uv[2][1]) * h->invdet;
+  h->V[1] = ((h->B[0] * uv[0][1] + h->B[1] * uv[1][1]) + h->B[2] * uv[2][1]) * h->invdet;
+  h->V[2] = ((h->C[0] * uv[0][1] + h->C[1] * uv[1][1]) + h->C[2] * uv[2][1]) * h->invdet;
+}
+
+static inline float plane_at(const float* P, float fx, float fy) { return (P[0] * fx + P[1] * fy) + P[2]; }
+
+/* 1/W at the pixel centre. */
+static inline float hom_invw(const hom_t* h, int px, int py) {
+  return plane_at(h->D, (float)px + 0.5f, (float)py + 0.5f);
 }
 
 /* Bilinear RGBA8 fetch, repeat wrap, 8-bit fixed weights. */
@@ -134,11 +150,11 @@ static void tri_clip_coords(const inst_ctx* ic, uint32_t t, cv3 v[3], float uv[3
   }
 }
 
-static inline void interp_uv(const float e[3], float s, const float uv[3][2], float* u, float* v) {
-  const float rs = 1.0f / s;
-  const float l0 = e[0] * rs, l1 = e[1] * rs, l2 = e[2] * rs;
-  *u = (l0 * uv[0][0] + l1 * uv[1][0]) + l2 * uv[2][0];
-  *v = (l0 * uv[0][1] + l1 * uv[1][1]) + l2 * uv[2][1];
+/* Texture coordinates at the pixel centre: u = U(x, y) * (1 / (1/W)). */
+static inline void interp_uv(const hom_t* h, int px, int py, float invw, float* u, float* v) {
+  const float fx = (float)px + 0.5f, fy = (float)py + 0.5f, r = 1.0f / invw;
+  *u = plane_at(h->U, fx, fy) * r;
+  *v = plane_at(h->V, fx, fy) * r;
 }
 
 /* Label coverage for occlusion: per label, the pixels a
@@ -153,12 +169,12 @@ typedef struct {
   uint32_t n_labels, tiles_x, tiles_y;
 } cov_t;
 
-static int alpha_passes(const oracle_scene* s, const oracle_material* mat, const float e[3], float ssum,
-                        const float uv[3][2]) {
+static int alpha_passes(const oracle_scene* s, const oracle_material* mat, const hom_t* h, int px, int py,
+                        float invw) {
   if (!(mat->alpha_test && mat->texture >= 0)) return 1;
   float u, v;
   int c[4];
-  interp_uv(e, ssum, uv, &u, &v);
+  interp_uv(h, px, py, invw, &u, &v);
   tex_sample(s, mat->texture, u, v, c);
   return c[3] > (int)mat->alpha_threshold;
 }
@@ -166,7 +182,7 @@ static int alpha_passes(const oracle_scene* s, const oracle_material* mat, const
 /* Rasterise one screen triangle (fixed point) for the original triangle `uid`. */
 static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3], const float sv[3],
                        const hom_t* h, uint32_t uid, const oracle_material* mat,
-                       const float uv[3][2], oracle_stats* st, cov_t* cv) {
+                       oracle_stats* st, cov_t* cv) {
   const int W = (int)s->width, H = (int)s->height;
   int32_t x[3], y[3];
   for (int k = 0; k < 3; ++k) {
@@ -216,13 +232,12 @@ static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3],
       }
       if (!inside) continue;
       st->n_covered++;
-      float e[3], ssum, invw;
-      hom_eval(h, px, py, e, &ssum, &invw);
+      const float invw = hom_invw(h, px, py);
       if (!(invw >= inv_far && invw <= inv_near)) continue;
       st->n_fragments++;
       if (cv) {
         const int32_t lab = s->inst_label[uid >> UID_SHIFT];
-        if (lab >= 0 && (uint32_t)lab < cv->n_labels && alpha_passes(s, mat, e, ssum, uv)) {
+        if (lab >= 0 && (uint32_t)lab < cv->n_labels && alpha_passes(s, mat, h, px, py, invw)) {
           const size_t bit = (size_t)lab * W * H + (size_t)py * W + px;
           cv->bits[bit >> 3] |= (uint8_t)(1u << (bit & 7));
           cv->tile[((size_t)(py / COV_TILE) * cv->tiles_x + px / COV_TILE) * cv->n_labels + lab] = 1;
@@ -235,7 +250,7 @@ static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3],
         st->n_alpha_tests++;
         float u, v;
         int c[4];
-        interp_uv(e, ssum, uv, &u, &v);
+        interp_uv(h, px, py, invw, &u, &v);
         tex_sample(s, mat->texture, u, v, c);
         if (!(c[3] > (int)mat->alpha_threshold)) { st->n_alpha_killed++; continue; }
       }
@@ -393,6 +408,7 @@ int oracle_render_frame_cov(const oracle_scene* s, const float* view, const floa
       hom_t h;
       hom_setup(v, &h);
       if (!h.ok) { st.n_culled++; continue; }
+      hom_planes(&h, uv);
       const uint32_t uid = (i << UID_SHIFT) | t;
       const int all_in = v[0].w >= near && v[1].w >= near && v[2].w >= near;
       if (all_in) {
@@ -402,7 +418,7 @@ int oracle_render_frame_cov(const oracle_scene* s, const float* view, const floa
           su[k] = v[k].x * rw;
           sv[k] = v[k].y * rw;
         }
-        raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st, cv);
+        raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, &st, cv);
       } else {
         /* Sutherland-Hodgman against W >= near, edges v0->v1, v1->v2, v2->v0 */
         st.n_clipped++;
@@ -429,7 +445,7 @@ int oracle_render_frame_cov(const oracle_scene* s, const float* view, const floa
             su[k] = tri3[k].x * rw;
             sv[k] = tri3[k].y * rw;
           }
-          raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, uv, &st, cv);
+          raster_tri(s, zbuf, su, sv, &h, uid, ic.mat, &st, cv);
         }
       }
     }
@@ -474,8 +490,8 @@ int oracle_render_frame_cov(const oracle_scene* s, const float* view, const floa
       tri_clip_coords(&ic, t, v, uv);
       hom_t h;
       hom_setup(v, &h);
-      float e[3], ssum, invw;
-      hom_eval(&h, px, py, e, &ssum, &invw);
+      hom_planes(&h, uv);
+      const float invw = hom_invw(&h, px, py);
       const int32_t label = s->inst_label[i];
       if (depth) depth[p] = 1.0f / invw;
       if (points) unproject(cam, px, py, 1.0f / invw, points + p * 3);
@@ -494,7 +510,7 @@ int oracle_render_frame_cov(const oracle_scene* s, const float* view, const floa
       if (mat->texture >= 0 && ic.m->has_uv) {
         float u, vv;
         int c[4];
-        interp_uv(e, ssum, uv, &u, &vv);
+        interp_uv(&h, px, py, invw, &u, &vv);
         tex_sample(s, mat->texture, u, vv, c);
         for (int k = 0; k < 3; ++k) alb[k] = (c[k] * mat->base[k] + 127) / 255;
       } else {
