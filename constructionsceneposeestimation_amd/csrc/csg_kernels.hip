@@ -929,10 +929,10 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 //
 // Occupancy: k_raster is latency-bound (LDS and VMEM dependency chains), and
 // waves per SIMD are its lever (measured on C3 against 4 waves: 3 waves +22%
-// time, 5 waves -8%, 6 waves a further -5%; 7 and 8 waves lose again to the
-// smaller batches and shade tables they need).  Six 256-thread workgroups per
-// CU need <= 26 KiB of LDS each (128 staged records, 128 shade-table slots)
-// and <= 80 VGPRs.
+// time, 5 waves -8%, 6 waves a further -5%; with 96-B records 7 waves a
+// further -4%, 8 waves lose again to spills and small batches).  Seven
+// 256-thread workgroups per CU need <= 22 KiB of LDS each (104 staged records,
+// 116 shade-table slots) and <= 72 VGPRs.
 #ifndef CSG_RASTER_FRAME_FAST
 #define CSG_RASTER_FRAME_FAST 0
 #endif
@@ -946,16 +946,16 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 #define CSG_TILE_SWIZZLE 2
 #endif
 #ifndef CSG_STAGE
-#define CSG_STAGE 128
+#define CSG_STAGE 104
 #endif
 #ifndef CSG_WAVES
-#define CSG_WAVES 6             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
+#define CSG_WAVES 7             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
 #endif
 #ifndef CSG_COV_STAGE
-#define CSG_COV_STAGE 88        // k_raster<true>: smaller batches pay for the coverage table (6 workgroups per CU)
+#define CSG_COV_STAGE 64        // k_raster<true>: smaller batches pay for the coverage table (7 workgroups per CU)
 #endif
 #ifndef CSG_COV_WAVES
-#define CSG_COV_WAVES 6
+#define CSG_COV_WAVES 7
 #endif
 #if CSG_WAVES > 0
 #define CSG_RASTER_ATTR \
@@ -1474,7 +1474,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
 // triangles in an open-addressing table of kShadeSlots, each set up once by
 // one thread, then read by every pixel that shows it.
 #ifndef CSG_SHADE_SLOTS
-#define CSG_SHADE_SLOTS 128
+#define CSG_SHADE_SLOTS 116
 #endif
 constexpr uint32_t kShadeSlots = CSG_SHADE_SLOTS;   // <= kBlock (one setup thread per slot)
 static_assert(kShadeSlots <= (uint32_t)kBlock && kShadeSlots < 255u, "one setup thread per slot; 8-bit slot ids");
@@ -1490,7 +1490,7 @@ struct ResolveLds {
 // (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4;
 // 26,656 B keeps 6.)
 constexpr size_t lds_budget(int waves) {
-  return waves >= 7 ? 22528u : waves == 6 ? 26700u : waves == 5 ? 32256u : 40960u;
+  return waves >= 8 ? 20480u : waves == 7 ? 22528u : waves == 6 ? 26700u : waves == 5 ? 32256u : 40960u;
 }
 static_assert((sizeof(RasterLds<kStage>) > sizeof(ResolveLds) ? sizeof(RasterLds<kStage>) : sizeof(ResolveLds)) +
                       kTilePix * 8 <= lds_budget(CSG_WAVES),
@@ -1604,7 +1604,7 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
 // kCov: also the per-label coverage for occlusion (b.covered); a separate
 // instantiation launched only when the caller asks for it.  Its coverage table
 // (4.1 KiB) is paid for with smaller batches (CSG_COV_STAGE records), so it
-// keeps 6 workgroups per CU.
+// keeps 7 workgroups per CU.
 template <bool kCov>
 __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, BatchDev b) {
   __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
