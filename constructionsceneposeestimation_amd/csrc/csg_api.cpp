@@ -865,6 +865,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       HIP_TRY(c, hipMemsetAsync(c->drange.p, 0xFF, sizeof(uint32_t) * Fc, st));
       HIP_TRY(c, hipMemsetAsync(c->drange.p + Fc, 0, sizeof(uint32_t) * Fc, st));
     }
+    bc.drange = (CSG_FUSED_RANGE && want_dvis) ? c->drange.p : nullptr;   // reduced by k_raster's resolve
+    bc.drange_F = Fc;
     if (c->timing) {
       const uint32_t slot = (uint32_t)(c->ring_count % csg_ctx::kRing);
       c->ev = &c->ring[(size_t)slot * 5];
@@ -886,7 +888,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (out->depth_stats)
       launch_depth_stats(bc.depth, (uint32_t)npx, Fc, c->dstat_part.p, dstats + (size_t)c0 * 6, st);
     if (want_dvis) {
-      launch_depth_range(bc.depth, (uint32_t)npx, Fc, c->drange.p, st);
+      if (!CSG_FUSED_RANGE) launch_depth_range(bc.depth, (uint32_t)npx, Fc, c->drange.p, st);
       if (dvis || drange_out) {
         uint8_t* vo = dvis ? dvis + (size_t)c0 * npx * 3 : nullptr;
         float* ro = drange_out ? drange_out + (size_t)c0 * 2 : nullptr;

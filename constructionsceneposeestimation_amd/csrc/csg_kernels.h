@@ -18,6 +18,9 @@ constexpr uint32_t kCovUnknown = 0x80000000u;   // covered[] flag: a tile held m
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
 constexpr uint32_t kNoAlpha = 0xFFFFFFFFu;  // Rec::atex of a record without alpha test
 constexpr uint32_t kCamFloats = 16;         // per-frame unprojection constants (frame_camera)
+#ifndef CSG_FUSED_RANGE
+#define CSG_FUSED_RANGE 1   // the depth visualisation's per-frame min / max come from k_raster's resolve
+#endif
 
 struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };   // host-side bookkeeping
 // Per instance, everything a kernel needs before touching its triangles (one load).
@@ -126,6 +129,8 @@ struct BatchDev {
   uint32_t* kp_pix;            // [F][K] px | py << 16 of in-view keypoints, else ~0
   uint32_t* kp_tiles;          // [F][tile_words] bitmap of tiles holding an in-view keypoint
   uint32_t tile_words;
+  uint32_t* drange;            // [2][drange_F] min / max bits of the valid depths of each frame, reduced by
+  uint32_t drange_F;           //   k_raster's resolve (null: not wanted; CSG_FUSED_RANGE)
   uint32_t dbg;                // ablation switches for profiling only (CSG_DEBUG env; 0 in production)
 };
 

@@ -1713,15 +1713,35 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   unsigned long long* zrow = &zb[ly * kTile + lx0];
   uint32_t pend = 0;                 // bit k: pixel k still to shade
   uint32_t inmask = 0;               // bit k: pixel k lies inside the frame
+  // The depth visualisation's range (b.drange), from the winning keys: the
+  // written depth is 1/invW (IEEE, monotone), so the tile's smallest depth is
+  // 1/(largest invW), i.e. comes from the smallest key.  Reduced per wave here;
+  // thread 0 combines the waves after the first round's barrier.
+  __shared__ uint32_t drw[2][kBlock / 64];
   {
     const uint32_t sky = b.lights[b.fset[f]].sky & 0xFFFFFFu;
     const unsigned long long bgword = (unsigned long long)sky | (0xFFFFFFFFull << 32);   // id -1
+    uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;   // key high words (0xFFFFFFFF - bits(invW))
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool in = row_ok && px0 + k < (int)s.W;
       inmask |= in ? 1u << k : 0u;
-      if (in && zrow[k] != kEmptyKey) pend |= 1u << k;
-      else zrow[k] = bgword;         // background (or outside the frame)
+      const unsigned long long key = zrow[k];
+      if (in && key != kEmptyKey) {
+        pend |= 1u << k;
+        kmn = min(kmn, (uint32_t)(key >> 32));
+        kmx = max(kmx, (uint32_t)(key >> 32));
+      } else {
+        zrow[k] = bgword;            // background (or outside the frame)
+      }
+    }
+    if (b.drange) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        kmn = min(kmn, (uint32_t)__shfl_xor((int)kmn, o, 64));
+        kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, o, 64));
+      }
+      if ((tid & 63) == 0) { drw[0][tid >> 6] = kmn; drw[1][tid >> 6] = kmx; }
     }
   }
   const size_t npx = (size_t)s.W * s.H;
@@ -1740,6 +1760,18 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     // every thread has read the previous round's flag (it reached this
     // barrier) and none sets it before the next barrier
     if (tid == 0) L.q.more = 0;
+    if (first && b.drange && tid == 0) {   // the tile's depth range (see drw)
+      uint32_t kmn = drw[0][0], kmx = drw[1][0];
+#pragma unroll
+      for (int w = 1; w < kBlock / 64; ++w) { kmn = min(kmn, drw[0][w]); kmx = max(kmx, drw[1][w]); }
+      if (kmn <= kmx) {   // some pixel has a surface: depths 1/invW, valid (finite, > 0) by the depth range test
+        const float dmin = 1.0f / __uint_as_float(0xFFFFFFFFu - kmn);
+        const float dmax = 1.0f / __uint_as_float(0xFFFFFFFFu - kmx);
+        // skip the atomic when the frame's range already holds it (most tiles)
+        if (__float_as_uint(dmin) < b.drange[f]) atomicMin(&b.drange[f], __float_as_uint(dmin));
+        if (__float_as_uint(dmax) > b.drange[b.drange_F + f]) atomicMax(&b.drange[b.drange_F + f], __float_as_uint(dmax));
+      }
+    }
     uint32_t slots = 0xFFFFFFFFu;    // 8 bits per pixel (0xFF: none this round)
     {
       uint32_t prev_uid = 0xFFFFFFFFu, prev_slot = 0xFFu;
