@@ -406,10 +406,20 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
     }
     const int nw = px1 - px0, nh = py1 - py0;
     uint32_t cols = 0, rows = 0;
+    // the active lanes' largest box, wave-uniform: a wave of 1x1 and 2x2 boxes
+    // evaluates 1 or 4 centres, not N*N
+    int nwm = 0, nhm = 0;
+#pragma unroll
+    for (int k = 1; k < N; ++k) {
+      nwm += __any(nw >= k) ? 1 : 0;
+      nhm += __any(nh >= k) ? 1 : 0;
+    }
 #pragma unroll
     for (int j = 0; j < N; ++j) {
+      if (j > nhm) break;
 #pragma unroll
       for (int i = 0; i < N; ++i) {
+        if (i > nwm) break;
         bool in = i <= nw && j <= nh;
 #pragma unroll
         for (int e = 0; e < 3; ++e) in &= e0[e] + sx[e] * i + sy[e] * j >= 0;
