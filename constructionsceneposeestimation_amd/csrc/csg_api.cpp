@@ -125,6 +125,7 @@ struct csg_ctx {
   DevBuf<float> clip, pv;
   DevBuf<Rec> recs;
   DevBuf<uint32_t> rect, rec_count, tile_count, tile_off, tile_fill, bins, overflow;
+  DevBuf<uint32_t> bcount;              // [chain frames][bin_blocks][n_tiles] count grid (CSG_BIN_GRID)
   // internal outputs (host-output mode / scratch)
   DevBuf<uint8_t> o_rgb;
   DevBuf<int32_t> o_inst;
@@ -162,7 +163,7 @@ struct csg_ctx {
   hipEvent_t* ev = nullptr;             // events of the most recent batch
   uint32_t last_F = 0;
   uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
-  uint32_t bin_blocks = 128;            // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only)
+  uint32_t bin_blocks = 32;             // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only)
   uint32_t chain_frames = 0;            // frames per launch chain (cfg.frames_per_launch; CSG_CHAIN overrides)
 
   int fail(int code, const char* fmt, ...) {
@@ -301,7 +302,7 @@ void csg_destroy(csg_ctx* c) {
   c->acls.release();
   c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
   c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
-  c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->overflow.release(); c->o_rgb.release();
+  c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->bcount.release(); c->overflow.release(); c->o_rgb.release();
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
   c->kp_w.release(); c->kp_pix.release(); c->kp_tiles.release();
   c->o_points.release(); c->o_normals.release(); c->cam.release(); c->fset.release();
@@ -680,6 +681,7 @@ static int ensure_work(csg_ctx* c) {
   HIP_TRY(c, c->tile_off.alloc((size_t)maxF * (c->n_tiles + 1)));
   HIP_TRY(c, c->tile_fill.alloc((size_t)maxF * c->n_tiles));
   HIP_TRY(c, c->bins.alloc((size_t)maxF * c->bin_cap));
+  if (CSG_BIN_GRID) HIP_TRY(c, c->bcount.alloc((size_t)maxF * c->bin_blocks * c->n_tiles));
   c->work_frames = maxF;
   return CSG_OK;
 }
@@ -754,6 +756,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   b.rec_cap = c->rec_cap;
   b.rec_count = c->rec_count.p;
   b.tile_count = c->tile_count.p;
+  b.bcount = c->bcount.p;
+  b.bin_blocks = c->bin_blocks;
   b.tile_off = c->tile_off.p;
   b.tile_fill = c->tile_fill.p;
   b.bins = c->bins.p;
@@ -856,8 +860,10 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       bc.kp_vis += (size_t)c0 * c->n_kp;
     }
     HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * Fc * kCounterStride, st));
-    HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
-    HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
+    if (!CSG_BIN_GRID) {   // (the count grid needs neither: k_colscan writes every tile count)
+      HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
+      HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
+    }
     if (want_kp) HIP_TRY(c, hipMemsetAsync(bc.kp_tiles, 0, sizeof(uint32_t) * Fc * bc.tile_words, st));
     launch_init_stats(bc, Fc, st);
     if (bc.covered) HIP_TRY(c, hipMemsetAsync(bc.covered, 0, sizeof(uint32_t) * Fc * b.n_labels, st));
@@ -878,6 +884,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     launch_setup(s, bc, c->chunks.p, c->n_chunks, Fc, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
     launch_count(s, bc, Fc, c->bin_blocks, st);
+    if (CSG_BIN_GRID) launch_colscan(s, bc, Fc, st);
     launch_scan(s, bc, Fc, st);
     launch_bin(s, bc, Fc, c->bin_blocks, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));

@@ -18,6 +18,9 @@ constexpr uint32_t kCovUnknown = 0x80000000u;   // covered[] flag: a tile held m
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
 constexpr uint32_t kNoAlpha = 0xFFFFFFFFu;  // Rec::atex of a record without alpha test
 constexpr uint32_t kCamFloats = 16;         // per-frame unprojection constants (frame_camera)
+#ifndef CSG_BIN_GRID
+#define CSG_BIN_GRID 1      // bin offsets from a [blocks][tiles] count grid (no global atomics in k_bin)
+#endif
 #ifndef CSG_FUSED_RANGE
 #define CSG_FUSED_RANGE 1   // the depth visualisation's per-frame min / max come from k_raster's resolve
 #endif
@@ -110,6 +113,9 @@ struct BatchDev {
   uint32_t* tile_fill;         // [F][n_tiles]
   uint32_t* bins;              // [F][bin_cap]
   uint32_t bin_cap;
+  uint32_t* bcount;            // [F][bin_blocks][n_tiles] (CSG_BIN_GRID): each k_count block's tile counts,
+                               //   then (k_colscan) the block's first slot in each tile's list, tile-relative
+  uint32_t bin_blocks;
   uint32_t* overflow;          // [16]: [0] bit0 rec, bit1 bins; [1..] profiling counters (CSG_DEBUG 512)
   // outputs (device)
   uint8_t* rgb;                // [F][H][W][3] or null
@@ -140,6 +146,7 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
                   uint32_t F, hipStream_t st);
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
+void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);   // CSG_BIN_GRID
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 // depth visualisation (GDP:1690-1709): per-frame min / max of the valid depth

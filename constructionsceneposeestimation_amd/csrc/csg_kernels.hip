@@ -764,11 +764,34 @@ __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
     }
     __syncthreads();
   }
+#if CSG_BIN_GRID
+  // this block's row of the count grid (k_colscan turns it into offsets)
+  uint32_t* bc = b.bcount + ((size_t)f * gridDim.x + blockIdx.x) * s.n_tiles;
+  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) bc[t] = hist[t];
+#else
   uint32_t* tc = b.tile_count + (size_t)f * s.n_tiles;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) {
     const uint32_t c = hist[t];
     if (c) atomicAdd(&tc[t], c);
   }
+#endif
+}
+
+// Column scan of the count grid: per tile, the exclusive prefix over the
+// k_count blocks (in block order, so each block's entries of a tile take a
+// fixed range of its list) and the tile's total.  Grid (tile groups, F).
+__global__ __launch_bounds__(256) void k_colscan(SceneDev s, BatchDev b) {
+  const uint32_t f = blockIdx.y, t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= s.n_tiles) return;
+  uint32_t* col = b.bcount + (size_t)f * b.bin_blocks * s.n_tiles + t;
+  uint32_t run = 0;
+#pragma unroll 8
+  for (uint32_t k = 0; k < b.bin_blocks; ++k) {
+    const uint32_t v = col[(size_t)k * s.n_tiles];
+    col[(size_t)k * s.n_tiles] = run;
+    run += v;
+  }
+  b.tile_count[(size_t)f * s.n_tiles + t] = run;
 }
 
 // ---------------------------------------------------------------------------
@@ -805,7 +828,9 @@ __global__ __launch_bounds__(256) void k_scan(SceneDev s, BatchDev b) {
 __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   extern __shared__ uint32_t dyn[];
   uint32_t* hist = dyn;                  // [n_tiles]
+#if !CSG_BIN_GRID
   uint32_t* tbase = dyn + s.n_tiles;     // [n_tiles]
+#endif
   __shared__ uint32_t pre[kBinRound + 1];
   __shared__ uint32_t lrc[kBinRound];
   __shared__ uint32_t wsum[kBlock / 64];
@@ -814,8 +839,26 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   const uint32_t n = min(b.rec_count[f * kCounterStride], b.rec_cap);
   const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
-  uint32_t* fill = b.tile_fill + (size_t)f * s.n_tiles;
   uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
+#if CSG_BIN_GRID
+  // Each tile's next free slot for this block: the tile's list start plus the
+  // entries of the blocks before it (k_colscan).  No global atomics.
+  const uint32_t* bo = b.bcount + ((size_t)f * gridDim.x + blockIdx.x) * s.n_tiles;
+  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = toff[t] + bo[t];
+  __syncthreads();
+  for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
+    const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
+    __syncthreads();
+    for (uint32_t j = tid; j < total; j += kBlock) {
+      const int k = find_bin_item(pre, j);
+      const uint32_t slot = atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
+      if (slot < b.bin_cap) bins[slot] = base + (uint32_t)k;
+    }
+    __syncthreads();
+  }
+}
+#else
+  uint32_t* fill = b.tile_fill + (size_t)f * s.n_tiles;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
@@ -845,6 +888,7 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
     __syncthreads();
   }
 }
+#endif
 
 // Exact range [xl, xr] (tile-local, clamped to [x0, x1]) of the pixels on row
 // `ly` whose centres R covers.  Per edge, in tile-relative fixed point,
@@ -2200,7 +2244,11 @@ void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t s
 
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
   dim3 g(blocks, F);
-  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), 2 * s.n_tiles * sizeof(uint32_t), st, s, b);
+  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), (CSG_BIN_GRID ? 1 : 2) * s.n_tiles * sizeof(uint32_t), st, s, b);
+}
+
+void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
+  hipLaunchKernelGGL(k_colscan, dim3((s.n_tiles + kBlock - 1) / kBlock, F), dim3(kBlock), 0, st, s, b);
 }
 
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
