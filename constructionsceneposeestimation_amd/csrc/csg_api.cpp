@@ -78,6 +78,7 @@ struct csg_ctx {
   std::vector<MeshDesc> h_meshes;
   DevBuf<Chunk> chunks;
   uint32_t n_chunks = 0;
+  uint32_t uid_shift = kUidShift;       // SceneDev::uid_shift
   std::vector<HostTexture> textures;
   bool tex_dirty = true;
   DevBuf<uint8_t> texels;
@@ -367,6 +368,13 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   }
   // de-index: one 9-float position record and one 6-float uv record per triangle
   const size_t n_soup = tris.size() / 3;
+  {  // kernel uids: instance << uid_shift | soup index (SceneDev::uid_shift)
+    uint32_t shift = kUidShift;
+    while (shift < 31 && (1ull << shift) < n_soup) ++shift;
+    if ((1ull << shift) < n_soup || (uint64_t)n_inst > (1ull << (32 - shift)))
+      return c->fail(CSG_ERR_LIMIT, "upload_scene: %zu soup triangles x %u instances exceed 32-bit uids", n_soup, n_inst);
+    c->uid_shift = shift;
+  }
   std::vector<float> tri_pos(n_soup * 9), tri_uv(n_soup * 6, 0.f);
   for (uint32_t m = 0; m < n_meshes; ++m) {
     const MeshDesc& d = md[m];
@@ -695,6 +703,7 @@ static SceneDev scene_dev(const csg_ctx* c) {
   s.near_clip = c->cfg.near_clip; s.far_clip = c->cfg.far_clip;
   s.inv_near = 1.0f / c->cfg.near_clip; s.inv_far = 1.0f / c->cfg.far_clip;
   s.dbg = c->dbg;
+  s.uid_shift = c->uid_shift;
   return s;
 }
 

@@ -9,7 +9,7 @@ namespace csg {
 constexpr int kTile = 32;                 // screen tile edge (pixels)
 constexpr int kTilePix = kTile * kTile;   // 1024 pixels, one 256-thread workgroup
 constexpr int kBlock = 256;
-constexpr uint32_t kUidShift = 20;        // uid = (instance << 20) | triangle
+constexpr uint32_t kUidShift = 20;        // spec: uid = (instance << 20) | triangle (tie order); see SceneDev::uid_shift
 constexpr uint32_t kMaxInstances = 1u << (32 - kUidShift);
 constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
 constexpr int kMaxLdsLabels = 256;        // per-label pixel stats kept in LDS
@@ -85,6 +85,11 @@ struct SceneDev {
   float near_clip, far_clip;
   float inv_near, inv_far;     // 1/near_clip, 1/far_clip (IEEE, computed on the host)
   uint32_t dbg;                // ablation switches (CSG_DEBUG; 0 in production)
+  // Kernel uids are (instance << uid_shift) | (soup index of the triangle):
+  // the same order as the spec's (instance << 20) | mesh triangle (within an
+  // instance the soup index is the mesh's base plus the triangle), and the
+  // resolve finds the triangle without loading the instance first.
+  uint32_t uid_shift;
 };
 
 // Bits of overflow[0] (sticky until csg_synchronize / csg_render_batch reads them)

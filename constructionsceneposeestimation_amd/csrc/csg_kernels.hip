@@ -539,7 +539,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
       ob &= v[k].y > Hf * v[k].w;
     }
     if (!(on | of | ol | orr | ot | ob)) {
-      const uint32_t uid = (i << kUidShift) | t;
+      const uint32_t uid = (i << s.uid_shift) | (m.tbase + t);
       // Sutherland-Hodgman against W >= near over edges v0->v1, v1->v2, v2->v0
       // (each edge emits [start vertex if inside][intersection if crossing]),
       // written as a closed-form case table on the inside mask so the polygon
@@ -1260,7 +1260,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
       if (tid < NS) {
         int32_t lab = -1;
         if (rows) {
-          lab = s.inst[L.img.q[2][tid].x >> kUidShift].label;
+          lab = s.inst[L.img.q[2][tid].x >> s.uid_shift].label;
           if (lab >= 0 && (uint32_t)lab >= b.n_labels) lab = -1;
         }
         c.rlabel[tid] = lab;
@@ -1401,10 +1401,10 @@ struct ShadeEntry {
 // values are live at once (this phase sets the kernel's register budget).
 __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b, uint32_t f, uint32_t uid,
                                             ShadeEntry& e) {
-  const uint32_t i = uid >> kUidShift, t = uid & (kMaxTrisPerMesh - 1u);
+  const uint32_t i = uid >> s.uid_shift, g = uid & ((1u << s.uid_shift) - 1u);   // instance, soup index
   const uint32_t set = b.fset[f];
   const InstDesc m = s.inst[i];
-  const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
+  const float* tp = s.tri_pos + (size_t)g * 9;
   float p[9];
 #pragma unroll
   for (int z = 0; z < 9; ++z) p[z] = tp[z];
@@ -1413,7 +1413,7 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   const int tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
   e.tex = tex;
   e.base = (uint32_t)mat.base[0] | ((uint32_t)mat.base[1] << 8) | ((uint32_t)mat.base[2] << 16);
-  const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
+  const float* tu = s.tri_uv + (size_t)g * 6;
 #pragma unroll
   for (int z = 0; z < 6; ++z) e.P[10 + z] = tex >= 0 ? tu[z] : 0.0f;
   // Homogeneous coefficients: for texture coordinates, depth / points and the
