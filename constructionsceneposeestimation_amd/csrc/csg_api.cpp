@@ -127,6 +127,8 @@ struct csg_ctx {
   DevBuf<Rec> recs;
   DevBuf<uint32_t> rect, rec_count, tile_count, tile_off, tile_fill, bins, overflow;
   DevBuf<uint32_t> bcount;              // [chain frames][bin_blocks][n_tiles] count grid (CSG_BIN_GRID)
+  DevBuf<InstSetDev> iset;              // [n_table_sets][n_inst] resolved materials (sync_scene_state)
+  std::vector<InstDesc> h_inst;         // host copy of the instance table
   // internal outputs (host-output mode / scratch)
   DevBuf<uint8_t> o_rgb;
   DevBuf<int32_t> o_inst;
@@ -296,7 +298,7 @@ void csg_destroy(csg_ctx* c) {
   if (!c) return;
   if (c->last_stream && c->last_stream != c->stream) (void)hipStreamSynchronize(c->last_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->set_mats.release(); c->lights.release();
+  c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->set_mats.release(); c->iset.release(); c->lights.release();
   c->chunks.release();
   c->texels.release();
   c->aquad.release();
@@ -420,6 +422,8 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   HIP_TRY(c, hipMemcpy(c->tri_pos.p, tri_pos.data(), tri_pos.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->tri_uv.p, tri_uv.data(), tri_uv.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->inst.p, idesc.data(), idesc.size() * sizeof(InstDesc), hipMemcpyHostToDevice));
+  c->h_inst = idesc;
+  c->iset.release();   // rebuilt for the new instances by the next sync_scene_state
   HIP_TRY(c, hipMemcpy(c->chunks.p, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice));
   c->n_inst = n_inst;
   c->n_meshes = n_meshes;
@@ -584,6 +588,7 @@ static int sync_scene_state(csg_ctx* c) {
     if (rc) return rc;
   }
   const bool tex_changed = c->tex_dirty;
+  const bool iset_dirty = c->tex_dirty || c->dr_dirty || c->n_table_sets != n_sets || !c->iset.p;
   const bool cls_dirty = c->tex_dirty || c->dr_dirty || c->n_table_sets != n_sets || !c->acls.p;
   std::vector<TexDesc> td(c->textures.size());
   size_t total = 0;
@@ -644,6 +649,29 @@ static int sync_scene_state(csg_ctx* c) {
     if (t >= 0 && ((size_t)t >= c->textures.size() || !c->textures[t].present))
       return c->fail(CSG_ERR_INVALID, "material %u (set %u) references texture %d that was not uploaded",
                      (unsigned)(k % c->n_materials), (unsigned)(k / c->n_materials), t);
+  }
+  if (iset_dirty) {   // each instance's material per set, texture descriptors inlined
+    std::vector<InstSetDev> is((size_t)n_sets * c->n_inst);
+    for (uint32_t set = 0; set < n_sets; ++set)
+      for (uint32_t i = 0; i < c->n_inst; ++i) {
+        const InstDesc& d = c->h_inst[i];
+        const MatDesc& m = c->h_set_mats[(size_t)set * c->n_materials + d.material];
+        InstSetDev e{};
+        e.tex = (m.texture >= 0 && d.has_uv) ? m.texture : -1;
+        e.base = (uint32_t)m.base[0] | ((uint32_t)m.base[1] << 8) | ((uint32_t)m.base[2] << 16);
+        e.atex = kNoAlpha;
+        if (m.alpha_test && m.texture >= 0) {
+          const TexDesc& t = td[(size_t)m.texture];
+          e.atex = t.offset;
+          e.atex_wh = t.width | (t.height << 16);
+          e.athr = m.alpha_threshold;
+        }
+        e.label = d.label;
+        e.alpha_uv = (m.alpha_test && d.has_uv) ? 1u : 0u;
+        is[(size_t)set * c->n_inst + i] = e;
+      }
+    HIP_TRY(c, c->iset.alloc(std::max<size_t>(is.size(), 1)));
+    if (!is.empty()) HIP_TRY(c, hipMemcpy(c->iset.p, is.data(), is.size() * sizeof(InstSetDev), hipMemcpyHostToDevice));
   }
   if (c->models_dirty) {
     HIP_TRY(c, c->models.alloc(c->h_models.size()));
@@ -755,6 +783,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   b.n_kp_sets = (uint32_t)c->kp_valid.size();
   b.models = c->models.p;
   b.mats = c->set_mats.p;
+  b.iset = c->iset.p;
   b.lights = c->lights.p;
   b.n_mat = c->n_materials;
   b.clip = c->clip.p;

@@ -29,6 +29,20 @@ struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };   /
 // Per instance, everything a kernel needs before touching its triangles (one load).
 struct InstDesc { uint32_t tbase, material, has_uv; int32_t label; };
 struct MatDesc { uint8_t base[4]; int32_t texture; uint32_t alpha_test, alpha_threshold; };
+// One instance's material in one transform set, resolved on the host (texture
+// swaps applied, texture descriptor inlined): k_setup and the resolve read it
+// with one load that depends only on (set, instance).
+struct InstSetDev {
+  int32_t tex;        // texture sampled by the resolve (-1: flat albedo; also -1 without uvs)
+  uint32_t base;      // albedo multiplier r | g << 8 | b << 16
+  uint32_t atex;      // alpha test: texel offset of the texture (kNoAlpha: none)
+  uint32_t atex_wh;   // alpha texture width | height << 16
+  uint32_t athr;      // alpha threshold
+  int32_t label;      // the instance's label
+  uint32_t alpha_uv;  // alpha-tested material on a mesh with uvs (the record carries uv planes)
+  uint32_t pad;
+};
+static_assert(sizeof(InstSetDev) == 32, "InstSetDev layout");
 struct TexDesc { uint32_t offset, width, height, pad; };
 // Lighting of one transform set (randomisation epoch): dome (ambient) and
 // distant-light contributions per channel, unit direction toward the sun,
@@ -105,6 +119,7 @@ struct BatchDev {
   uint32_t n_kp_sets;          // keypoint sets resident
   const float* models;         // [n_sets][I][16]
   const MatDesc* mats;         // [n_sets][n_mat] materials with the set's texture swaps applied
+  const InstSetDev* iset;      // [n_sets][n_inst] each instance's resolved material per set
   const LightDev* lights;      // [n_sets]
   uint32_t n_mat;
   float* clip;                 // [F][I][12] rows 0,1,3 of P*V*M

@@ -598,17 +598,11 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
         if (!h.ok) {
           nrec = 0;
         } else {
-          const MatDesc mat = b.mats[(size_t)b.fset[f] * b.n_mat + m.material];
-          uint32_t atex = kNoAlpha, atex_wh = 0, athr = 0;
-          if (mat.alpha_test && mat.texture >= 0) {
-            const TexDesc td = s.texd[mat.texture];
-            atex = td.offset;
-            atex_wh = td.width | (td.height << 16);
-            athr = mat.alpha_threshold;
-          }
+          const InstSetDev is = b.iset[(size_t)b.fset[f] * s.n_inst + i];
+          const uint32_t atex = is.atex, atex_wh = is.atex_wh, athr = is.athr;
           float D[3], U[3] = {0.0f, 0.0f, 0.0f}, V[3] = {0.0f, 0.0f, 0.0f};
           depth_plane(h.A, h.B, h.C, h.invdet, D);
-          if (mat.alpha_test && m.has_uv) {   // uvs loaded only now: few values live at once
+          if (is.alpha_uv) {   // uvs loaded only now: few values live at once
             const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
             float uv[6];
 #pragma unroll
@@ -1403,16 +1397,15 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
                                             ShadeEntry& e) {
   const uint32_t i = uid >> s.uid_shift, g = uid & ((1u << s.uid_shift) - 1u);   // instance, soup index
   const uint32_t set = b.fset[f];
-  const InstDesc m = s.inst[i];
   const float* tp = s.tri_pos + (size_t)g * 9;
   float p[9];
 #pragma unroll
   for (int z = 0; z < 9; ++z) p[z] = tp[z];
-  e.label = m.label;
-  const MatDesc mat = b.mats[(size_t)set * b.n_mat + m.material];
-  const int tex = (mat.texture >= 0 && m.has_uv) ? mat.texture : -1;
+  const InstSetDev is = b.iset[(size_t)set * s.n_inst + i];   // (independent of the triangle loads)
+  e.label = is.label;
+  const int tex = is.tex;
   e.tex = tex;
-  e.base = (uint32_t)mat.base[0] | ((uint32_t)mat.base[1] << 8) | ((uint32_t)mat.base[2] << 16);
+  e.base = is.base;
   const float* tu = s.tri_uv + (size_t)g * 6;
 #pragma unroll
   for (int z = 0; z < 6; ++z) e.P[10 + z] = tex >= 0 ? tu[z] : 0.0f;
