@@ -404,6 +404,7 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
       c0.inst = i;
       c0.start = s0;
       c0.count = std::min<uint32_t>(kBlock, nt - s0);
+      c0.soup = md_i.tbase + s0;   // soup index of the chunk's first triangle
       for (int a = 0; a < 3; ++a) { c0.lo[a] = INFINITY; c0.hi[a] = -INFINITY; }
       for (uint32_t t = s0; t < s0 + c0.count; ++t)
         for (int k = 0; k < 3; ++k) {

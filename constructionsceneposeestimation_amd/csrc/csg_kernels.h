@@ -49,7 +49,8 @@ struct TexDesc { uint32_t offset, width, height, pad; };
 // background colour r | g << 8 | b << 16.
 struct LightDev { float ambient[3], sun[3], sun_dir[3]; uint32_t sky; };
 struct Chunk {                    // <= 256 triangles of one instance + their object-space AABB
-  uint32_t inst, start, count, pad;
+  uint32_t inst, start, count;
+  uint32_t soup;                  // soup index of triangle `start` (the mesh's base + start)
   float lo[3], hi[3];
   uint32_t pad2[2];
 };

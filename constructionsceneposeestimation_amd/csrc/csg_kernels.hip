@@ -512,12 +512,11 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   uint4 c2 = make_uint4(0u, 0u, 0u, 0u), c3 = c2, c4 = c2, c5 = c2;
   int nrec = 0;
   if ((uint32_t)tid < ch.count) {
-    const uint32_t t = ch.start + tid;
+    const uint32_t g = ch.soup + tid;   // soup index (no instance-table load on the way)
     float c[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) c[k] = Cm[k];
-    const InstDesc m = s.inst[i];
-    const float* tp = s.tri_pos + (size_t)(m.tbase + t) * 9;
+    const float* tp = s.tri_pos + (size_t)g * 9;
     Cv3 v[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -539,7 +538,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
       ob &= v[k].y > Hf * v[k].w;
     }
     if (!(on | of | ol | orr | ot | ob)) {
-      const uint32_t uid = (i << s.uid_shift) | (m.tbase + t);
+      const uint32_t uid = (i << s.uid_shift) | g;
       // Sutherland-Hodgman against W >= near over edges v0->v1, v1->v2, v2->v0
       // (each edge emits [start vertex if inside][intersection if crossing]),
       // written as a closed-form case table on the inside mask so the polygon
@@ -603,7 +602,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
           float D[3], U[3] = {0.0f, 0.0f, 0.0f}, V[3] = {0.0f, 0.0f, 0.0f};
           depth_plane(h.A, h.B, h.C, h.invdet, D);
           if (is.alpha_uv) {   // uvs loaded only now: few values live at once
-            const float* tu = s.tri_uv + (size_t)(m.tbase + t) * 6;
+            const float* tu = s.tri_uv + (size_t)g * 6;
             float uv[6];
 #pragma unroll
             for (int k = 0; k < 6; ++k) uv[k] = tu[k];
@@ -2066,7 +2065,7 @@ __global__ __launch_bounds__(256) void k_inst_bounds(SceneDev s, const Chunk* __
     float m[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) m[k] = M[k];
-    const float* tp = s.tri_pos + (size_t)(s.inst[i].tbase + ch.start + tid) * 9;
+    const float* tp = s.tri_pos + (size_t)(ch.soup + tid) * 9;
 #pragma unroll
     for (int v = 0; v < 3; ++v) {
       const float x = tp[3 * v], y = tp[3 * v + 1], z = tp[3 * v + 2];
