@@ -58,6 +58,9 @@ namespace csg {
 #ifndef CSG_ALPHA_CLASS
 #define CSG_ALPHA_CLASS 1      // alpha tests decided by the 2-bit quad class where it can (see alpha_pass)
 #endif
+#ifndef CSG_BIN_REVERSE
+#define CSG_BIN_REVERSE 1       // each tile's list holds its records in reverse append order (raster -0.8% on C3)
+#endif
 #ifndef CSG_SMALL_COVER
 #define CSG_SMALL_COVER 4      // records with at most N x N pixel centres get an exact cover test in k_setup (0: off)
 #endif
@@ -837,14 +840,27 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   // Each tile's next free slot for this block: the tile's list start plus the
   // entries of the blocks before it (k_colscan).  No global atomics.
   const uint32_t* bo = b.bcount + ((size_t)f * gridDim.x + blockIdx.x) * s.n_tiles;
+#if CSG_BIN_REVERSE
+  // Reverse append order: this block's range mirrored, filled from its end.
+  // Outputs do not depend on the order (the z-buffer minimum and the coverage
+  // bits are order-independent); the raster is measurably faster this way.
+  const uint32_t* tcnt = b.tile_count + (size_t)f * s.n_tiles;
+  for (uint32_t t = tid; t < s.n_tiles; t += kBlock)
+    hist[t] = toff[t] + tcnt[t] - bo[t] - 1u;   // last slot of the mirrored range; decremented
+#else
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = toff[t] + bo[t];
+#endif
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
     const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
       const int k = find_bin_item(pre, j);
+#if CSG_BIN_REVERSE
+      const uint32_t slot = atomicSub(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
+#else
       const uint32_t slot = atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
+#endif
       if (slot < b.bin_cap) bins[slot] = base + (uint32_t)k;
     }
     __syncthreads();
