@@ -1550,7 +1550,7 @@ struct ResolveLds {
 
 // The resolve's LDS aliases the raster loop's in a union inside k_raster.
 // (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4;
-// 26,656 B keeps 6.)
+// 26,656 B keeps 6; 22,448 B keeps 7.)
 constexpr size_t lds_budget(int waves) {
   return waves >= 8 ? 20480u : waves == 7 ? 22528u : waves == 6 ? 26700u : waves == 5 ? 32256u : 40960u;
 }
