@@ -23,11 +23,11 @@ The line validates what it timed before it prints a number:
   aborts the run.  On rank 0 at N=1 the same oracle runs are the CPU
   baseline.
 
-Reported extras: ``roofline`` (B_frame x frames per launch /
-the average k_raster launch timed with HIP events on its stream, plus per-
-kernel entries and the frame-level fraction fps x B_frame / peak) and
-``cpu_baseline`` (oracle/csg_oracle.c, a port of the same arithmetic -- the
-reference has no CPU render path -- single-thread and all-cores, median of 5
+Reported extras: ``roofline`` (BASELINE.md:44 / SURVEY §8(d): fps x B_frame
+/ 8 TB/s, plus per-kernel entries priced against the average launch of each
+kernel timed with HIP events on its stream) and ``cpu_baseline``
+(oracle/csg_oracle.c, a port of the same arithmetic -- the reference has no
+CPU render path -- single-thread and on the box's CPU share, median of 5
 after a warm-up, wall clock without file I/O).
 """
 from __future__ import annotations
@@ -122,14 +122,16 @@ def median_time(fn: Callable[[], None], runs: int = 5, warmup: int = 1, what: st
 
 def roofline(b_geom: int, b_tex: int, b_out: int, frames_per_launch: float, raster_ms: float, setup_ms: float,
              records_per_frame: float, fps: float, traffic: Optional[Dict[str, int]] = None) -> dict:
-    """B_frame = B_geom + B_tex + B_out per frame.  The headline
-    entry prices B_frame x frames per launch against the dominant kernel's
-    (k_raster) average launch; per-kernel entries price each kernel's own
-    algorithmic bytes; ``frame_level`` is fps x B_frame / peak."""
+    """SURVEY §8(d) / BASELINE.md:44: B_frame = B_geom + B_tex + B_out per
+    frame, and the headline fraction is ``fps x B_frame / 8 TB/s`` with fps
+    the per-GPU rate of the timed steps.  ``kernels`` prices the dominant
+    kernel (k_raster, whose average launch the HIP events on its stream
+    measure; rocprofv3 in profiles/ agrees) two ways -- its own algorithmic
+    bytes (B_out + B_tex) and the whole B_frame per launch -- and k_setup by
+    its own bytes."""
     traffic = traffic or {}
     b_frame = b_geom + b_tex + b_out
-    bpl = int(round(frames_per_launch * b_frame))
-    achieved = bpl / (raster_ms * 1e-3) / 1e9
+    achieved = fps * b_frame / 1e9
 
     def kern(name, nbytes, ms, what):
         a = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -139,18 +141,21 @@ def roofline(b_geom: int, b_tex: int, b_out: int, frames_per_launch: float, rast
 
     kernels = [
         kern("k_raster", round(frames_per_launch * (b_tex + b_out)), raster_ms,
-             "B_out + B_tex: outputs written once, bound textures read once"),
+             "own bytes: B_out + B_tex (outputs written once, bound textures read once) per launch"),
+        kern("k_raster", round(frames_per_launch * b_frame), raster_ms,
+             "B_frame x frames per launch against k_raster's launch alone (the round-2 headline; it counts "
+             "B_geom, which k_setup reads)"),
         kern("k_setup", round(b_geom + frames_per_launch * records_per_frame * RECORD_BYTES), setup_ms,
              "B_geom once per launch (the launch's frames share the geometry through L2 and the Infinity "
              "Cache: the grid runs frame-fast) + 100 B written per raster record (k_clip + k_setup)"),
     ]
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic.get("k_raster"), "kernel": "k_raster",
-            "bytes_per_launch": bpl, "avg_launch_ms": round(raster_ms, 4),
-            "formula": "B_frame (SURVEY §8(d)) x frames per launch / k_raster average launch (HIP events on its stream)",
-            "kernels": kernels,
-            "frame_level": {"B_frame": int(b_frame), "B_geom": int(b_geom), "B_tex": int(b_tex), "B_out": int(b_out),
-                            "frac": round(fps * b_frame / (HBM_PEAK_GBS * 1e9), 5)}}
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic.get("k_raster"),
+            "kernel": "k_raster", "avg_launch_ms": round(raster_ms, 4), "frames_per_launch": frames_per_launch,
+            "formula": "fps (per GPU, timed steps) x B_frame / 8 TB/s (BASELINE.md:44, SURVEY §8(d)); "
+                       "traffic = k_raster's PMC HBM bytes per launch",
+            "B_frame": int(b_frame), "B_geom": int(b_geom), "B_tex": int(b_tex), "B_out": int(b_out),
+            "kernels": kernels}
 
 
 def cpu_model() -> str:
@@ -187,22 +192,24 @@ class Verifier:
         self.extra = any(k in wl.outputs for k in ("normals", "points"))
 
     def render(self, frames: List[int], threads: int):
-        """(rgb, inst, depth[, normals, points]) of ``frames``; frames of DR
-        epochs (C4) or with C5 outputs are rendered one by one."""
+        """(rgb, inst, depth[, normals, points]) of ``frames`` on ``threads``
+        CPU threads: OpenMP over frames in the C oracle, or -- for frames of DR
+        epochs (C4, per-frame light and textures) and the C5 outputs -- one
+        oracle state per frame rendered on a thread pool."""
         wl, o = self.wl, self.o
         v, p = wl.frame_params(frames)
         if not wl.dr and not self.extra:
             models = np.stack([wl.epoch(f // 10).models.reshape(-1, 16) for f in frames])
             rgb, inst, depth = o.render_many(v, p, threads=threads, outputs=True, models=models)
             return v, p, {"rgb": rgb, "instance": inst, "depth": depth}
-        outs = {}
+        jobs = []
         for k, f in enumerate(frames):
             st = wl.epoch(f // 10)
-            o.set_instance_models(st.models.reshape(-1, 16))
-            if st.dr is not None:
-                o.set_light(st.dr.light)
-                o.set_material_textures(st.dr.textures)
-            r = o.render(v[k], p[k], extra=self.extra)
+            dr = st.dr
+            jobs.append((o.frame_state(st.models.reshape(-1, 16), dr.light if dr is not None else None,
+                                       dr.textures if dr is not None else None), v[k], p[k]))
+        outs = {}
+        for r in o.render_parallel(jobs, threads, extra=self.extra):
             for key, a in r.items():
                 if key != "inst_stats":
                     outs.setdefault(key, []).append(a)
@@ -397,11 +404,18 @@ def main():
             t_one = median_time(lambda: ver.render(sample_frames[:n1], 1), runs=5, warmup=1, what="1 thread")
             v_, p_, ref = res["out"]
             bad = ver.compare(sample_frames, v_, p_, ref, gpu_sample)
+            how = ("OpenMP over frames" if not (wl.dr or ver.extra) else
+                   "a thread pool of per-frame oracle states (DR light/textures or C5 outputs)")
             cpu = {"value": round(len(sample_frames) / t_all, 3), "unit": "frames/s", "cores": thr, "kind": "port",
                    "single_thread": round(n1 / t_one, 3),
+                   "share": (f"{thr} of the {available_cpus()} CPUs this process may use: the GPU box's CPU share "
+                             f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')})"
+                             if os.environ.get("OMP_NUM_THREADS") and not args.cpu_threads else
+                             f"{thr} of the {available_cpus()} CPUs this process may use"),
                    "sample": f"{len(sample_frames)} frames of the last timed step of the {args.workload} schedule "
-                             f"(seed {args.seed}) at {Wd}x{H} with {thr} OpenMP threads, {n1} of them single-threaded; "
-                             f"oracle/csg_oracle.c, median of 5 after 1 warm-up, wall clock, no file I/O",
+                             f"(seed {args.seed}) at {Wd}x{H} on {thr} threads ({how}); the first {n1} of them "
+                             f"also single-threaded; oracle/csg_oracle.c, median of 5 after 1 warm-up, wall clock, "
+                             f"no file I/O",
                    "method": "median of 5 after 1 warm-up", "nproc": os.cpu_count(), "available_cpus": available_cpus(),
                    "cpu_model": cpu_model()}
         else:

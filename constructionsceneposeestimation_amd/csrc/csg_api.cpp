@@ -125,8 +125,8 @@ struct csg_ctx {
   DevBuf<uint32_t> fset;                // [chain frames] checked transform set of each frame (k_clip)
   DevBuf<float> clip, pv;
   DevBuf<Rec> recs;
-  DevBuf<uint32_t> rect, rec_count, tile_count, tile_off, tile_fill, bins, overflow;
-  DevBuf<uint32_t> bcount;              // [chain frames][bin_blocks][n_tiles] count grid (CSG_BIN_GRID)
+  DevBuf<uint32_t> rect, rec_count, tile_count, tile_off, bins, overflow;
+  DevBuf<uint32_t> bcount;              // [chain frames][bin_blocks][n_tiles] count grid
   DevBuf<InstSetDev> iset;              // [n_table_sets][n_inst] resolved materials (sync_scene_state)
   std::vector<InstDesc> h_inst;         // host copy of the instance table
   // internal outputs (host-output mode / scratch)
@@ -140,7 +140,7 @@ struct csg_ctx {
   DevBuf<uint8_t> o_dvis;               // depth visualisation (host-output mode)
   DevBuf<float> o_drange;
   DevBuf<uint32_t> o_cov;               // label coverage (host-output mode)
-  DevBuf<uint32_t> drange;              // [2][chain frames] min / max depth bits (k_depth_range)
+  DevBuf<uint32_t> drange;              // [2][chain frames] min / max depth bits (k_raster's resolve)
   DevBuf<uint32_t> jet;                 // JET colour map, 256 x (r | g << 8 | b << 16)
   // images of the last batch (for the file encoders) and the encoders' buffers
   const uint8_t* last_rgb = nullptr;
@@ -210,7 +210,10 @@ static int take_flags(csg_ctx* c, uint32_t* flags_out) {
   }
   if (flags_out) *flags_out = ov;
   if (!ov) return CSG_OK;
-  HIP_TRY(c, hipMemset(c->overflow.p, 0, 4));
+  // cleared on the context stream and waited for: the next batch (on any
+  // stream) is enqueued only after the clear has landed
+  HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, 4, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (ov & (kOvBadSet | kOvBadKpSet))
     return c->fail(CSG_ERR_INVALID,
                    "device frame records named a transform set >= %u or a keypoint set >= %u (flags %u); those "
@@ -305,7 +308,7 @@ void csg_destroy(csg_ctx* c) {
   c->acls.release();
   c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
   c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
-  c->tile_off.release(); c->tile_fill.release(); c->bins.release(); c->bcount.release(); c->overflow.release(); c->o_rgb.release();
+  c->tile_off.release(); c->bins.release(); c->bcount.release(); c->overflow.release(); c->o_rgb.release();
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
   c->kp_w.release(); c->kp_pix.release(); c->kp_tiles.release();
   c->o_points.release(); c->o_normals.release(); c->cam.release(); c->fset.release();
@@ -716,9 +719,8 @@ static int ensure_work(csg_ctx* c) {
   HIP_TRY(c, c->rec_count.alloc((size_t)maxF * kCounterStride));
   HIP_TRY(c, c->tile_count.alloc((size_t)maxF * c->n_tiles));
   HIP_TRY(c, c->tile_off.alloc((size_t)maxF * (c->n_tiles + 1)));
-  HIP_TRY(c, c->tile_fill.alloc((size_t)maxF * c->n_tiles));
   HIP_TRY(c, c->bins.alloc((size_t)maxF * c->bin_cap));
-  if (CSG_BIN_GRID) HIP_TRY(c, c->bcount.alloc((size_t)maxF * c->bin_blocks * c->n_tiles));
+  HIP_TRY(c, c->bcount.alloc((size_t)maxF * c->bin_blocks * c->n_tiles));
   c->work_frames = maxF;
   return CSG_OK;
 }
@@ -798,7 +800,6 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   b.bcount = c->bcount.p;
   b.bin_blocks = c->bin_blocks;
   b.tile_off = c->tile_off.p;
-  b.tile_fill = c->tile_fill.p;
   b.bins = c->bins.p;
   b.bin_cap = c->bin_cap;
   b.overflow = c->overflow.p;
@@ -899,10 +900,6 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       bc.kp_vis += (size_t)c0 * c->n_kp;
     }
     HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * Fc * kCounterStride, st));
-    if (!CSG_BIN_GRID) {   // (the count grid needs neither: k_colscan writes every tile count)
-      HIP_TRY(c, hipMemsetAsync(c->tile_count.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
-      HIP_TRY(c, hipMemsetAsync(c->tile_fill.p, 0, sizeof(uint32_t) * Fc * c->n_tiles, st));
-    }
     if (want_kp) HIP_TRY(c, hipMemsetAsync(bc.kp_tiles, 0, sizeof(uint32_t) * Fc * bc.tile_words, st));
     launch_init_stats(bc, Fc, st);
     if (bc.covered) HIP_TRY(c, hipMemsetAsync(bc.covered, 0, sizeof(uint32_t) * Fc * b.n_labels, st));
@@ -910,7 +907,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       HIP_TRY(c, hipMemsetAsync(c->drange.p, 0xFF, sizeof(uint32_t) * Fc, st));
       HIP_TRY(c, hipMemsetAsync(c->drange.p + Fc, 0, sizeof(uint32_t) * Fc, st));
     }
-    bc.drange = (CSG_FUSED_RANGE && want_dvis) ? c->drange.p : nullptr;   // reduced by k_raster's resolve
+    bc.drange = want_dvis ? c->drange.p : nullptr;   // reduced by k_raster's resolve
     bc.drange_F = Fc;
     if (c->timing) {
       const uint32_t slot = (uint32_t)(c->ring_count % csg_ctx::kRing);
@@ -923,7 +920,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     launch_setup(s, bc, c->chunks.p, c->n_chunks, Fc, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
     launch_count(s, bc, Fc, c->bin_blocks, st);
-    if (CSG_BIN_GRID) launch_colscan(s, bc, Fc, st);
+    launch_colscan(s, bc, Fc, st);   // k_count's grid -> block offsets and tile counts
     launch_scan(s, bc, Fc, st);
     launch_bin(s, bc, Fc, c->bin_blocks, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[2], st));
@@ -934,7 +931,6 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     if (out->depth_stats)
       launch_depth_stats(bc.depth, (uint32_t)npx, Fc, c->dstat_part.p, dstats + (size_t)c0 * 6, st);
     if (want_dvis) {
-      if (!CSG_FUSED_RANGE) launch_depth_range(bc.depth, (uint32_t)npx, Fc, c->drange.p, st);
       if (dvis || drange_out) {
         uint8_t* vo = dvis ? dvis + (size_t)c0 * npx * 3 : nullptr;
         float* ro = drange_out ? drange_out + (size_t)c0 * 2 : nullptr;
@@ -1073,7 +1069,8 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
     uint32_t ov = 0;
     HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
     if (!ov) return fk ? encode_files(c, out, n_frames) : CSG_OK;
-    HIP_TRY(c, hipMemset(c->overflow.p, 0, 4));
+    HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, 4, c->stream));   // before the re-render, on its stream
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (ov & (kOvBadSet | kOvBadKpSet))   // host frames are validated before launch: cannot happen
       return c->fail(CSG_ERR_DEVICE, "render: unexpected set error flags %u", ov);
     // grow the overflowed capacity and re-render (results are a pure function

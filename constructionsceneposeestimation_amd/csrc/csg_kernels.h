@@ -18,12 +18,6 @@ constexpr uint32_t kCovUnknown = 0x80000000u;   // covered[] flag: a tile held m
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
 constexpr uint32_t kNoAlpha = 0xFFFFFFFFu;  // Rec::atex of a record without alpha test
 constexpr uint32_t kCamFloats = 16;         // per-frame unprojection constants (frame_camera)
-#ifndef CSG_BIN_GRID
-#define CSG_BIN_GRID 1      // bin offsets from a [blocks][tiles] count grid (no global atomics in k_bin)
-#endif
-#ifndef CSG_FUSED_RANGE
-#define CSG_FUSED_RANGE 1   // the depth visualisation's per-frame min / max come from k_raster's resolve
-#endif
 
 struct MeshDesc { uint32_t vbase, tbase, ntris, uvbase, has_uv, material; };   // host-side bookkeeping
 // Per instance, everything a kernel needs before touching its triangles (one load).
@@ -129,12 +123,11 @@ struct BatchDev {
   uint32_t* rect;              // [F][rec_cap] tile rect tx0|ty0<<8|tx1<<16|ty1<<24
   uint32_t rec_cap;
   uint32_t* rec_count;         // [F * kCounterStride] (one cache line per frame: no atomic contention)
-  uint32_t* tile_count;        // [F][n_tiles]
+  uint32_t* tile_count;        // [F][n_tiles] (k_colscan)
   uint32_t* tile_off;          // [F][n_tiles+1]
-  uint32_t* tile_fill;         // [F][n_tiles]
   uint32_t* bins;              // [F][bin_cap]
   uint32_t bin_cap;
-  uint32_t* bcount;            // [F][bin_blocks][n_tiles] (CSG_BIN_GRID): each k_count block's tile counts,
+  uint32_t* bcount;            // [F][bin_blocks][n_tiles]: each k_count block's tile counts,
                                //   then (k_colscan) the block's first slot in each tile's list, tile-relative
   uint32_t bin_blocks;
   uint32_t* overflow;          // [16]: [0] bit0 rec, bit1 bins; [1..] profiling counters (CSG_DEBUG 512)
@@ -157,7 +150,7 @@ struct BatchDev {
   uint32_t* kp_tiles;          // [F][tile_words] bitmap of tiles holding an in-view keypoint
   uint32_t tile_words;
   uint32_t* drange;            // [2][drange_F] min / max bits of the valid depths of each frame, reduced by
-  uint32_t drange_F;           //   k_raster's resolve (null: not wanted; CSG_FUSED_RANGE)
+  uint32_t drange_F;           //   k_raster's resolve (null: not wanted)
   uint32_t dbg;                // ablation switches for profiling only (CSG_DEBUG env; 0 in production)
 };
 
@@ -167,13 +160,12 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
                   uint32_t F, hipStream_t st);
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
-void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);   // CSG_BIN_GRID
+void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
-// depth visualisation (GDP:1690-1709): per-frame min / max of the valid depth
-// (range [2][F] as float bits: row 0 min, initialised to ~0; row 1 max, to 0),
-// then the JET-coloured RGB8 image; lut = 256 packed r | g << 8 | b << 16
-void launch_depth_range(const float* depth, uint32_t npx, uint32_t F, uint32_t* range, hipStream_t st);
+// depth visualisation (GDP:1690-1709): from the per-frame min / max of the valid
+// depth that k_raster reduced (range [2][F] as float bits: row 0 min, row 1 max),
+// the JET-coloured RGB8 image; lut = 256 packed r | g << 8 | b << 16
 void launch_depth_vis(const float* depth, uint32_t npx, uint32_t F, const uint32_t* range, const uint32_t* lut,
                       uint8_t* vis, float* range_out, hipStream_t st);
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st);

@@ -40,31 +40,12 @@ namespace csg {
 #define CSG_ABLATION 0         // 1: honour the CSG_DEBUG ablation / profiling bits (tools/ablate.sh builds)
 #endif
 #define DBG(d) (CSG_ABLATION ? (d) : 0u)
-#ifndef CSG_WRAP_FAST
-#define CSG_WRAP_FAST 1        // texel wrap: in-range coordinates skip the modulo (see wrap_index)
-#endif
-#ifndef CSG_TIGHT_ROWS
-#define CSG_TIGHT_ROWS 1       // staged row range widened by 1/16 px (not 1/2) for records near the tile
-#endif
-#ifndef CSG_SPAN_NOWALK
-#define CSG_SPAN_NOWALK 1      // row spans: exact walk only for boundaries within 1/64 px of a pixel centre
-#endif
-#ifndef CSG_HASH_XOR
-#define CSG_HASH_XOR 0         // shade-table hash: 1 = xor-fold, 0 = multiplicative (measured faster)
-#endif
-#ifndef CSG_OPAQUE_DIRECT
-#define CSG_OPAQUE_DIRECT 1    // opaque fragments go straight to ds_min_u64 (see fragment)
-#endif
-#ifndef CSG_ALPHA_CLASS
-#define CSG_ALPHA_CLASS 1      // alpha tests decided by the 2-bit quad class where it can (see alpha_pass)
-#endif
-#ifndef CSG_BIN_REVERSE
-#define CSG_BIN_REVERSE 1       // each tile's list holds its records in reverse append order (raster -0.8% on C3)
-#endif
-#ifndef CSG_SMALL_COVER
-#define CSG_SMALL_COVER 4      // records with at most N x N pixel centres get an exact cover test in k_setup (0: off)
-#endif
+// Every code path below is the production one (measured alternatives are in
+// DESIGN.md §6 "Measured and rejected"; tools/build_variant.sh rebuilds old
+// revisions for A/B).  The remaining macros are tuning constants of the same
+// code (CSG_STAGE, CSG_WAVES, ...), not alternative paths.
 
+constexpr int kSmallCover = 4;   // records with at most 4 x 4 pixel centres get an exact cover test in k_setup
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr float kGuardPx = 1048576.0f;
 
@@ -140,11 +121,9 @@ struct TexTap { uint32_t i00, i10, i01, i11; int wx, wy; };
 // it; q*n and fu - q*n are integers below 2^24, so every step is exact.
 __device__ __forceinline__ int wrap_index(float fu, int n) {
   const float nf = (float)n;
-#if CSG_WRAP_FAST
   // Texture coordinates inside one repeat (the usual case: uvs in [0, 1])
   // need no reduction; the branch is skipped when no lane of the wave wraps.
   if (fu >= 0.0f && fu < nf) return (int)fu;
-#endif
   const float q = floorf(fu * __builtin_amdgcn_rcpf(nf));
   float r = fu - q * nf;
   r += r < 0.0f ? nf : 0.0f;
@@ -219,10 +198,8 @@ __device__ __forceinline__ bool alpha_pass(const uint32_t* aquad, const uint32_t
   const float fu = floorf(tu), fv = floorf(tv);
   const uint32_t idx = offset + __umul24((uint32_t)wrap_index(fv, th) & 0x3FFFu, (uint32_t)tw & 0x7FFFu) +
                        ((uint32_t)wrap_index(fu, tw) & 0x3FFFu);   // (masks: see tex_taps)
-#if CSG_ALPHA_CLASS
   const uint32_t cl = (acls[idx >> 4] >> (2u * (idx & 15u))) & 3u;
   if (cl != 3u) return cl != 0u;
-#endif
   const int wx = (int)((tu - fu) * 256.0f) & 255, wy = (int)((tv - fv) * 256.0f) & 255;
   const uint32_t q = aquad[idx];
   return bilerp8(q & 255u, (q >> 8) & 255u, (q >> 16) & 255u, q >> 24, wx, wy) > thr;
@@ -266,19 +243,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   __syncthreads();
   total = tot;
   return off + inc - v;
-}
-
-// last k in [0,256) with pre[k] <= j  (pre has 257 entries, nondecreasing,
-// pre[0] <= j < pre[256]).  4-ary search: each step issues three independent
-// LDS reads, so the dependent chain is 4 LDS round trips instead of 8.
-__device__ __forceinline__ int find_item(const uint32_t* pre, uint32_t j) {
-  int lo = 0;
-#pragma unroll
-  for (int step = 64; step > 0; step >>= 2) {
-    const uint32_t a = pre[lo + step], b = pre[lo + 2 * step], c = pre[lo + 3 * step];
-    lo += ((a <= j) + (b <= j) + (c <= j)) * step;
-  }
-  return lo;
 }
 
 // Per-frame camera constants for unprojection (spec, same in csg_oracle.c):
@@ -387,14 +351,13 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
   px1 = min(px1, (int)s.W - 1);
   py1 = min(py1, (int)s.H - 1);
   if (px0 > px1 || py0 > py1) return false;
-#if CSG_SMALL_COVER
   // Small records (at most NxN pixel centres in the box, vertex extent below
   // 32 px): evaluate the spec's edge test at every centre of the box, drop the
   // record if it covers none and shrink the box to the covered pixels.  The
   // covered set is unchanged (so are the outputs); fewer, tighter records mean
   // fewer record stores, bin entries and raster row items.  Exact in int32:
   // |dx|, |dy| < 2^13 and every centre lies within the vertex extent.
-  constexpr int N = CSG_SMALL_COVER;
+  constexpr int N = kSmallCover;
   if (px1 - px0 < N && py1 - py0 < N && xmax - xmin < 8192 && ymax - ymin < 8192) {
     const int32_t cx0 = px0 * 256 + 128, cy0 = py0 * 256 + 128;
     const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
@@ -436,7 +399,6 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
     py1 = py0 + 31 - __clz(rows);
     py0 += __ffs(rows) - 1;
   }
-#endif
   r.g0 = make_uint4((uint32_t)x[0], (uint32_t)x[1], (uint32_t)x[2], (uint32_t)y[0]);
   r.g1 = make_uint4((uint32_t)y[1], (uint32_t)y[2], (uint32_t)px0 | ((uint32_t)py0 << 16),
                     (uint32_t)px1 | ((uint32_t)py1 << 16));
@@ -670,32 +632,26 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
 }
 
 // ---------------------------------------------------------------------------
-// Binning rounds.  A round takes kBinRpt records per thread (kBinRound per
+// Binning rounds.  A round takes kBinRpt = 4 records per thread (kBinRound per
 // block, each thread's records consecutive: one 16-B load of their tile
 // rects), scans their tile counts into pre[] and expands (record, tile) items
-// with a 4-ary search.  Bigger rounds mean fewer barriers, tile sweeps and --
-// in k_bin -- fewer rounds of latency-bound global reservations per block.
+// with a 4-ary search.  Bigger rounds mean fewer barriers and tile sweeps per
+// block (measured: 1 record per thread, bin +6%).
 // ---------------------------------------------------------------------------
-#ifndef CSG_BIN_RPT
-#define CSG_BIN_RPT 4
-#endif
-constexpr int kBinRpt = CSG_BIN_RPT;
+constexpr int kBinRpt = 4;
 constexpr uint32_t kBinRound = kBlock * kBinRpt;
-static_assert(kBinRpt == 1 || kBinRpt == 4, "records per thread per binning round");
 
-// last k in [0, kBinRound) with pre[k] <= j (pre: kBinRound + 1 entries, nondecreasing)
+// last k in [0, kBinRound) with pre[k] <= j (pre: kBinRound + 1 entries,
+// nondecreasing).  4-ary search: each step issues three independent LDS reads,
+// so the dependent chain is 5 LDS round trips instead of 10.
 __device__ __forceinline__ int find_bin_item(const uint32_t* pre, uint32_t j) {
-  if constexpr (kBinRpt == 1) {
-    return find_item(pre, j);
-  } else {
-    int lo = 0;
+  int lo = 0;
 #pragma unroll
-    for (int step = 256; step > 0; step >>= 2) {
-      const uint32_t a = pre[lo + step], b2 = pre[lo + 2 * step], c = pre[lo + 3 * step];
-      lo += ((a <= j) + (b2 <= j) + (c <= j)) * step;
-    }
-    return lo;
+  for (int step = 256; step > 0; step >>= 2) {
+    const uint32_t a = pre[lo + step], b2 = pre[lo + 2 * step], c = pre[lo + 3 * step];
+    lo += ((a <= j) + (b2 <= j) + (c <= j)) * step;
   }
+  return lo;
 }
 
 // Load this thread's records of the round at `base` (record ids base + tid*kBinRpt + q),
@@ -705,19 +661,16 @@ __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32
   const int tid = threadIdx.x;
   const uint32_t r0 = base + (uint32_t)tid * kBinRpt;
   uint32_t rc[kBinRpt], area[kBinRpt], sum = 0;
-  if constexpr (kBinRpt == 4) {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (r0 + 3 < n) {
-      v = *reinterpret_cast<const uint4*>(rect + r0);   // rect rows are 16-B aligned (rec_cap % 4 == 0)
-    } else {
-      if (r0 < n) v.x = rect[r0];
-      if (r0 + 1 < n) v.y = rect[r0 + 1];
-      if (r0 + 2 < n) v.z = rect[r0 + 2];
-    }
-    rc[0] = v.x; rc[1] = v.y; rc[2] = v.z; rc[3] = v.w;
+  static_assert(kBinRpt == 4, "one 16-B rect load per thread");
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (r0 + 3 < n) {
+    v = *reinterpret_cast<const uint4*>(rect + r0);   // rect rows are 16-B aligned (rec_cap % 4 == 0)
   } else {
-    rc[0] = r0 < n ? rect[r0] : 0u;
+    if (r0 < n) v.x = rect[r0];
+    if (r0 + 1 < n) v.y = rect[r0 + 1];
+    if (r0 + 2 < n) v.z = rect[r0 + 2];
   }
+  rc[0] = v.x; rc[1] = v.y; rc[2] = v.z; rc[3] = v.w;
 #pragma unroll
   for (int q = 0; q < kBinRpt; ++q) {
     area[q] = (r0 + (uint32_t)q < n) ? rect_area(rc[q]) : 0u;
@@ -760,17 +713,9 @@ __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
     }
     __syncthreads();
   }
-#if CSG_BIN_GRID
   // this block's row of the count grid (k_colscan turns it into offsets)
   uint32_t* bc = b.bcount + ((size_t)f * gridDim.x + blockIdx.x) * s.n_tiles;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) bc[t] = hist[t];
-#else
-  uint32_t* tc = b.tile_count + (size_t)f * s.n_tiles;
-  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) {
-    const uint32_t c = hist[t];
-    if (c) atomicAdd(&tc[t], c);
-  }
-#endif
 }
 
 // Column scan of the count grid: per tile, the exclusive prefix over the
@@ -819,14 +764,14 @@ __global__ __launch_bounds__(256) void k_scan(SceneDev s, BatchDev b) {
 }
 
 // ---------------------------------------------------------------------------
-// k_bin: scatter record ids into per-tile bins (LDS-aggregated atomics)
+// k_bin: scatter record ids into per-tile bins.  Each tile's next free slot
+// for this block comes from the count grid (the tile's list start plus the
+// entries of the blocks before it, k_colscan): LDS atomics only, no global
+// atomics, and each block's entries of a tile are a fixed range of its list.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   extern __shared__ uint32_t dyn[];
-  uint32_t* hist = dyn;                  // [n_tiles]
-#if !CSG_BIN_GRID
-  uint32_t* tbase = dyn + s.n_tiles;     // [n_tiles]
-#endif
+  uint32_t* hist = dyn;                  // [n_tiles] next slot of each tile
   __shared__ uint32_t pre[kBinRound + 1];
   __shared__ uint32_t lrc[kBinRound];
   __shared__ uint32_t wsum[kBlock / 64];
@@ -836,68 +781,27 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
   uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
-#if CSG_BIN_GRID
-  // Each tile's next free slot for this block: the tile's list start plus the
-  // entries of the blocks before it (k_colscan).  No global atomics.
   const uint32_t* bo = b.bcount + ((size_t)f * gridDim.x + blockIdx.x) * s.n_tiles;
-#if CSG_BIN_REVERSE
   // Reverse append order: this block's range mirrored, filled from its end.
   // Outputs do not depend on the order (the z-buffer minimum and the coverage
-  // bits are order-independent); the raster is measurably faster this way.
+  // bits are order-independent); the raster is measurably faster this way
+  // (-0.8% on C3: the scene's small foreground proxies, appended last, reach
+  // the z-buffer first).
   const uint32_t* tcnt = b.tile_count + (size_t)f * s.n_tiles;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock)
     hist[t] = toff[t] + tcnt[t] - bo[t] - 1u;   // last slot of the mirrored range; decremented
-#else
-  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = toff[t] + bo[t];
-#endif
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
     const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
       const int k = find_bin_item(pre, j);
-#if CSG_BIN_REVERSE
       const uint32_t slot = atomicSub(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
-#else
-      const uint32_t slot = atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
-#endif
       if (slot < b.bin_cap) bins[slot] = base + (uint32_t)k;
     }
     __syncthreads();
   }
 }
-#else
-  uint32_t* fill = b.tile_fill + (size_t)f * s.n_tiles;
-  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
-  __syncthreads();
-  for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-    const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
-    __syncthreads();
-    for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_bin_item(pre, j);
-      atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t t = tid; t < s.n_tiles; t += kBlock) {
-      const uint32_t c = hist[t];
-      if (c) {
-        tbase[t] = toff[t] + atomicAdd(&fill[t], c);
-        hist[t] = 0;
-      }
-    }
-    __syncthreads();
-    for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_bin_item(pre, j);
-      const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
-      const uint32_t slot = tbase[t] + atomicAdd(&hist[t], 1u);
-      if (slot < b.bin_cap) bins[slot] = base + (uint32_t)k;
-    }
-    __syncthreads();
-    for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
-    __syncthreads();
-  }
-}
-#endif
 
 // Exact range [xl, xr] (tile-local, clamped to [x0, x1]) of the pixels on row
 // `ly` whose centres R covers.  Per edge, in tile-relative fixed point,
@@ -936,7 +840,6 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
     lo = (dy < 0) ? fmaxf(lo, t) : lo;
     hi = (dy == 0 && c0[e] < 0) ? -1.0e30f : hi;
   }
-#if CSG_SPAN_NOWALK
   // Near the strip the float boundaries are within ~1e-5 px of the exact ones
   // (tile-relative values below 2^14 units, ~2^-22 relative error).  An end
   // whose boundary lies farther than kEps from every pixel centre is exact as
@@ -952,13 +855,6 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
   const float fl = lcc - floorf(lcc), fh = hcc - floorf(hcc);
   const bool walk_l = lc > (float)x0 - 0.5f && lc < (float)x1 + 0.5f && (fl <= kEps || fl >= 1.0f - kEps);
   const bool walk_r = hc > (float)x0 - 0.5f && hc < (float)x1 + 0.5f && (fh <= kEps || fh >= 1.0f - kEps);
-#else
-  const float l = fminf(fmaxf((lo - 128.0f) * (1.0f / 256.0f) - 0.0625f, (float)x0 - 1.0f), (float)x1 + 1.0f);
-  const float h = fmaxf(fminf((hi - 128.0f) * (1.0f / 256.0f) + 0.0625f, (float)x1 + 1.0f), (float)x0 - 1.0f);
-  xl = max((int)ceilf(l), x0);
-  xr = min((int)floorf(h), x1);
-  const bool walk_l = true, walk_r = true;
-#endif
   if (no_exact) return;   // ablation only (CSG_DEBUG 2048): superset span
   auto covers = [&](int lx) {
     const int32_t cx = lx * 256 + 128;
@@ -996,23 +892,11 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // further -4%, 8 waves lose again to spills and small batches).  Seven
 // 256-thread workgroups per CU need <= 22 KiB of LDS each (104 staged records,
 // 116 shade-table slots) and <= 72 VGPRs.
-#ifndef CSG_RASTER_FRAME_FAST
-#define CSG_RASTER_FRAME_FAST 0
-#endif
-#ifndef CSG_L1_BITMAP
-#define CSG_L1_BITMAP 1
-#endif
-#ifndef CSG_L2_BITMAP
-#define CSG_L2_BITMAP 1
-#endif
-#ifndef CSG_TILE_SWIZZLE
-#define CSG_TILE_SWIZZLE 2
-#endif
 #ifndef CSG_STAGE
 #define CSG_STAGE 104
 #endif
 #ifndef CSG_WAVES
-#define CSG_WAVES 7             // k_raster waves per SIMD to budget registers for (0: compiler's choice)
+#define CSG_WAVES 7             // k_raster waves per SIMD to budget registers for
 #endif
 #ifndef CSG_COV_STAGE
 #define CSG_COV_STAGE 64        // k_raster<true>: smaller batches pay for the coverage table (7 workgroups per CU)
@@ -1020,12 +904,8 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 #ifndef CSG_COV_WAVES
 #define CSG_COV_WAVES 7
 #endif
-#if CSG_WAVES > 0
 #define CSG_RASTER_ATTR \
   __attribute__((amdgpu_waves_per_eu(kCov ? CSG_COV_WAVES : CSG_WAVES, kCov ? CSG_COV_WAVES : CSG_WAVES)))
-#else
-#define CSG_RASTER_ATTR
-#endif
 constexpr int kStage = CSG_STAGE;     // records staged per raster batch (<= kBlock)
 static_assert(kStage <= kBlock && CSG_COV_STAGE <= kBlock, "one staged record per thread");
 template <bool kCov>
@@ -1141,14 +1021,12 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
     if (zwin) atomicMin(z, key);
     return;
   }
-#if CSG_OPAQUE_DIRECT
   // Without an alpha test the ds_min_u64 is the depth test: no early-z read,
   // compare and branch (a losing key leaves the word unchanged).
   if (g2.y == kNoAlpha && !(DBG(c.dbg) & 512u)) {
     atomicMin(z, key);
     return;
   }
-#endif
   if (!(DBG(c.dbg) & 16u) && key >= *z) {
     if (DBG(c.dbg) & 512u) atomicAdd(&c.ctr[7], 1u);   // profiling: early-z rejects
     return;
@@ -1214,14 +1092,10 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 #pragma unroll
   for (int k = 0; k < 3; ++k)
     small &= abs(X[k] - ox * 256) < (1 << 14) && abs(Y[k] - oy * 256) < (1 << 14);
-#if CSG_TIGHT_ROWS
   // Vertices within 64 px of the tile: every value above is below 2^16 units
   // and off by < 0.01 units, so a 1/16-px widening suffices (half a pixel
   // otherwise added about one empty row per record and tile).
   const float wid = small ? 16.0f : 128.0f;
-#else
-  const float wid = 128.0f;
-#endif
   const int r0 = (int)ceilf((ylo - 128.0f - wid) * (1.0f / 256.0f));
   const int r1 = (int)floorf((yhi - 128.0f + wid) * (1.0f / 256.0f));
   y0 = max(y0, oy + r0);
@@ -1233,21 +1107,13 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 template <int NS>
 struct RasterLds {
   RecImage<NS> img;                     // staged bin records
-#if CSG_L1_BITMAP
   uint32_t starts1[NS];                 // bit i: a staged record's rows start at level-1 item i
   uint16_t before1[NS + 1];             // records starting before item 32*d
   uint32_t crec[NS];                    // compact record: slot | first item << 8
-#else
-  uint32_t pre[kBlock + 1];             // row-item prefix per record
-#endif
   uint8_t row0[kBlock];                 // first tile row of each staged record | 0x80 if small
   uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
-#if CSG_L2_BITMAP
   uint32_t starts[kBlock];              // bit i: a span starts at level-2 item i (<= 256 spans x 32 px)
   uint16_t before[kBlock + 1];          // spans starting before item 32*d
-#else
-  uint32_t pre2[kBlock + 1];            // pixel-item prefix per span
-#endif
   uint32_t wsum[kBlock / 64];
 };
 
@@ -1284,7 +1150,6 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
         atomicAdd(&b.overflow[10], rows);   // ... their row items
       }
     }
-#if CSG_L1_BITMAP
     // records with rows get compact indices; item -> record is a rank query
     // over a bitmap of record starts (as for level 2 below)
     if (tid < NS) L.starts1[tid] = 0u;   // ordered before the atomics by the scan's barriers
@@ -1298,27 +1163,16 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
       atomicOr(&L.starts1[ex1 >> 5], 1u << (ex1 & 31u));
       if ((e_end & ~31u) > ex1) L.before1[e_end >> 5] = (uint16_t)(ci + 1u);
     }
-#else
-    uint32_t tot1;
-    const uint32_t ex1 = block_excl_scan(rows, L.wsum, tot1);
-    L.pre[tid] = ex1;
-    if (tid == kBlock - 1) L.pre[kBlock] = ex1 + rows;
-#endif
     __syncthreads();
     for (uint32_t c1 = 0; c1 < ((DBG(b.dbg) & 256u) ? 0u : tot1); c1 += kBlock) {
       const uint32_t j1 = c1 + tid;
       uint32_t w2 = 0, sp = 0;
       int xl = 0;
       if (j1 < tot1) {
-#if CSG_L1_BITMAP
         const uint32_t w1 = L.starts1[j1 >> 5], nb1 = L.before1[j1 >> 5];
         const uint32_t cr = L.crec[nb1 + (uint32_t)__popc(w1 & (0xFFFFFFFFu >> (31u - (j1 & 31u)))) - 1u];
         const int k = (int)(cr & 255u);
         const uint32_t first = cr >> 8;
-#else
-        const int k = find_item(L.pre, j1);
-        const uint32_t first = L.pre[k];
-#endif
         const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
         const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
         const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
@@ -1344,7 +1198,6 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
         if (((g1.w & 0xFFFFu) - (g1.z & 0xFFFFu)) < 4u && ((g1.w >> 16) - (g1.z >> 16)) < 4u)
           atomicAdd(&b.overflow[11], w2);   // level-2 items of records with at most 4 x 4 box
       }
-#if CSG_L2_BITMAP
       // Non-empty spans get compact indices (one packed scan gives item
       // offset and index).  Item -> span is then a rank query: a bitmap of
       // span starts plus, per 32-item word, the spans starting before it (the
@@ -1369,19 +1222,6 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
         fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
-#else
-      uint32_t tot2;
-      const uint32_t ex2 = block_excl_scan(w2, L.wsum, tot2);
-      L.span[tid] = sp | ((ex2 - (uint32_t)xl + 32u) << 16);
-      L.pre2[tid] = ex2;
-      if (tid == kBlock - 1) L.pre2[kBlock] = ex2 + w2;
-      __syncthreads();
-      for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kBlock) {
-        const uint32_t spj = L.span[find_item(L.pre2, j)];
-        fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
-      }
-      __syncthreads();
-#endif
     }
   }
 }
@@ -1576,13 +1416,7 @@ static_assert((sizeof(RasterSide<true>) > sizeof(ResolveLds) ? sizeof(RasterSide
 
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
 __device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
-#if CSG_HASH_XOR
-  // [0, kShadeSlots): xor-fold of the uid (shifts only)
-  static_assert((kShadeSlots & (kShadeSlots - 1)) == 0, "power-of-two table");
-  const uint32_t h = (uid ^ (uid >> 7) ^ (uid >> 14) ^ (uid >> 21)) & (kShadeSlots - 1u);
-#else
   const uint32_t h = __umulhi(uid * 2654435761u, kShadeSlots);   // [0, kShadeSlots)
-#endif
 #pragma clang loop vectorize(disable) unroll(disable)
   for (int p = 0; p < kShadeProbes; ++p) {
     uint32_t idx = h + (uint32_t)p;
@@ -1599,7 +1433,7 @@ __device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
 // square share one L2, so a record binned to several of them is fetched once,
 // while all XCDs keep working side by side on the same part of the frame.
 // Blocks past the frame's edge (odd tile counts) return at once.
-constexpr uint32_t kSq = CSG_TILE_SWIZZLE > 0 ? CSG_TILE_SWIZZLE : 1;   // square edge in tiles
+constexpr uint32_t kSq = 2;   // square edge in tiles
 __device__ __forceinline__ bool swizzled_tile(uint32_t v, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tile) {
   const uint32_t sqx = (tiles_x + kSq - 1) / kSq, sqy = (tiles_y + kSq - 1) / kSq;
   const uint32_t sq = (v / (8u * kSq * kSq)) * 8u + (v & 7u), j = (v >> 3) % (kSq * kSq);
@@ -1671,24 +1505,14 @@ template <bool kCov>
 __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, BatchDev b) {
   __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
   constexpr int NS = kStageOf<kCov>;
-#ifdef CSG_LDS_PAD
-  __shared__ volatile uint32_t ldspad[CSG_LDS_PAD / 4];   // A/B only: occupancy probe
-  if (b.dbg == 0xDEADu) ldspad[threadIdx.x] = 1u;
-#endif
   __shared__ union Lds {
     RasterSide<kCov> ra;                             // raster loop
     ResolveLds q;                                    // resolve
   } L;
   const int tid = threadIdx.x;
-#if CSG_RASTER_FRAME_FAST
-  const uint32_t tile = blockIdx.y, f = blockIdx.x;
-#elif CSG_TILE_SWIZZLE
   uint32_t tile;
   if (!swizzled_tile(blockIdx.x, s.tiles_x, s.tiles_y, tile)) return;
   const uint32_t f = blockIdx.y;
-#else
-  const uint32_t tile = blockIdx.x, f = blockIdx.y;
-#endif
   const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
   const uint32_t beg = min(toff[tile], b.bin_cap);
@@ -2125,52 +1949,11 @@ __global__ void k_project(const float* pts, uint32_t n, const float* pv, float W
 // ---------------------------------------------------------------------------
 // Depth visualisation (GDP:1690-1709): the reference normalises the valid
 // depth (finite, > 0) of each frame by its min / max and maps it through
-// OpenCV's JET colour map.  Two streaming passes over the depth image
-// (HBM-bound): a per-frame min / max reduction, then the colour lookup.
-// Valid depths are positive floats, so their bit patterns order like the
-// values and the reduction runs on u32 atomics.
+// OpenCV's JET colour map.  The per-frame min / max come from k_raster's
+// resolve (b.drange: the winning keys' depths, reduced per tile); this pass
+// streams the depth image once for the colour lookup (HBM-bound).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool depth_valid(float d) { return d > 0.0f && d < INFINITY; }
-
-template <bool kVec>
-__global__ __launch_bounds__(256) void k_depth_range(const float* __restrict__ depth, uint32_t npx,
-                                                     uint32_t* __restrict__ range, uint32_t F) {
-  const uint32_t f = blockIdx.y;
-  const float* d = depth + (size_t)f * npx;
-  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-  auto take = [&](float v) {
-    if (depth_valid(v)) {
-      mn = min(mn, __float_as_uint(v));
-      mx = max(mx, __float_as_uint(v));
-    }
-  };
-  const uint32_t stride = gridDim.x * blockDim.x;
-  if constexpr (kVec) {   // npx % 4 == 0 and a 16-B aligned base: every frame starts aligned
-    const float4* d4 = reinterpret_cast<const float4*>(d);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npx / 4u; i += stride) {
-      const float4 v = d4[i];
-      take(v.x); take(v.y); take(v.z); take(v.w);
-    }
-  } else {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += stride) take(d[i]);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
-  }
-  __shared__ uint32_t wmn[4], wmx[4];
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { wmn[w] = mn; wmx[w] = mx; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < 4; ++k) { mn = min(mn, wmn[k]); mx = max(mx, wmx[k]); }
-    if (mn != 0xFFFFFFFFu) {
-      atomicMin(&range[f], mn);
-      atomicMax(&range[F + f], mx);
-    }
-  }
-}
 
 // Index of one depth value (GDP:1698-1700, NumPy 1.x promotion as Isaac Sim
 // runs it): (depth_max - depth_min) is a float32 scalar, + 1e-6 promotes it to
@@ -2252,7 +2035,7 @@ void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t s
 
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
   dim3 g(blocks, F);
-  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), (CSG_BIN_GRID ? 1 : 2) * s.n_tiles * sizeof(uint32_t), st, s, b);
+  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), s.n_tiles * sizeof(uint32_t), st, s, b);
 }
 
 void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
@@ -2260,14 +2043,8 @@ void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_
 }
 
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
-#if CSG_RASTER_FRAME_FAST
-  dim3 g(F, s.n_tiles);
-#elif CSG_TILE_SWIZZLE
   const uint32_t squares = ((s.tiles_x + kSq - 1) / kSq) * ((s.tiles_y + kSq - 1) / kSq);
   dim3 g(8 * kSq * kSq * ((squares + 7) / 8), F);
-#else
-  dim3 g(s.n_tiles, F);
-#endif
   if (b.covered) hipLaunchKernelGGL(k_raster<true>, g, dim3(kBlock), 0, st, s, b);
   else hipLaunchKernelGGL(k_raster<false>, g, dim3(kBlock), 0, st, s, b);
 }
@@ -2292,15 +2069,6 @@ void launch_inst_bounds(const SceneDev& s, const Chunk* chunks, uint32_t n_chunk
 void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip, float* uv,
                     int32_t* vis, hipStream_t st) {
   hipLaunchKernelGGL(k_project, dim3((n + 255) / 256), dim3(256), 0, st, pts, n, pv12, W, H, near_clip, uv, vis);
-}
-
-void launch_depth_range(const float* depth, uint32_t npx, uint32_t F, uint32_t* range, hipStream_t st) {
-  const bool vec = (npx % 4u) == 0 && ((uintptr_t)depth & 15u) == 0;
-  const uint32_t per = vec ? npx / 4u : npx;
-  const uint32_t blocks = std::min<uint32_t>(64u, (per + 4095u) / 4096u);   // ~16 items per thread at 1080p
-  dim3 g(blocks ? blocks : 1u, F);
-  if (vec) hipLaunchKernelGGL(k_depth_range<true>, g, dim3(256), 0, st, depth, npx, range, F);
-  else hipLaunchKernelGGL(k_depth_range<false>, g, dim3(256), 0, st, depth, npx, range, F);
 }
 
 void launch_depth_vis(const float* depth, uint32_t npx, uint32_t F, const uint32_t* range, const uint32_t* lut,

@@ -33,8 +33,9 @@
  *   csg_copy_files / csg_host_alloc / csg_host_free (pinned buffers for them)
  *   csg_last_error / csg_destroy
  *
- * Threading: one context per device per process; a context is not
- * thread-safe.  No global state.
+ * Threading: several contexts may share a device (each has its own stream
+ * and work buffers; the generator drives two from two threads); a context is
+ * used by one thread at a time.  No global state.
  */
 #ifndef CSG_API_H
 #define CSG_API_H

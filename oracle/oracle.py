@@ -166,6 +166,33 @@ class Oracle:
             out["stats"] = {n: int(getattr(st, n)) for n, _ in _Stats._fields_}
         return out
 
+    def frame_state(self, models16: Optional[np.ndarray] = None, light=None, texture_per_material=None) -> "Oracle":
+        """A shallow copy that renders with its own instance models, light and
+        material textures (the scene arrays are shared): one per frame of a
+        DR batch, so frames of different epochs can render on parallel threads."""
+        o = Oracle.__new__(Oracle)
+        o.p, o.width, o.height = self.p, self.width, self.height
+        o._keep = list(self._keep)
+        o.s = _Scene()
+        C.memmove(C.addressof(o.s), C.addressof(self.s), C.sizeof(_Scene))
+        if models16 is not None:
+            o.set_instance_models(models16)
+        if light is not None:
+            o.set_light(light)
+        if texture_per_material is not None:
+            o.set_material_textures(texture_per_material)
+        return o
+
+    def render_parallel(self, jobs, threads: int, extra: bool = False):
+        """Render ``jobs`` = [(oracle_state, view, proj)] on ``threads`` Python
+        threads (each ctypes call releases the GIL; oracle_render_frame_cov is
+        reentrant); returns the per-frame output dicts in order."""
+        from concurrent.futures import ThreadPoolExecutor
+        if threads <= 1:
+            return [o.render(v, p, extra=extra) for o, v, p in jobs]
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            return list(ex.map(lambda j: j[0].render(j[1], j[2], extra=extra), jobs))
+
     def keypoints(self, view, proj, pts: np.ndarray, depth: np.ndarray):
         pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
         uv = np.empty((pts.shape[0], 2), np.float32)

@@ -48,14 +48,17 @@ def test_roofline_formula_follows_survey_8d():
     r = bench.roofline(b_geom=1000 * M, b_tex=200 * M, b_out=300 * M, frames_per_launch=10, raster_ms=2.0,
                        setup_ms=1.0, records_per_frame=5 * M, fps=1000.0, traffic={"k_raster": 99})
     b_frame = 1500 * M
-    assert r["bytes_per_launch"] == 10 * b_frame
-    assert r["achieved"] == pytest.approx(10 * b_frame / 2e-3 / 1e9, rel=1e-3)
-    assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, rel=1e-3)
-    assert r["traffic"] == 99 and r["bound"] == "hbm" and r["unit"] == "GB/s"
-    ks = {k["kernel"]: k for k in r["kernels"]}
-    assert ks["k_raster"]["bytes_per_launch"] == 10 * (200 + 300) * M
-    assert ks["k_setup"]["bytes_per_launch"] == (1000 + 10 * 5 * bench.RECORD_BYTES) * M   # geometry once per launch
-    assert r["frame_level"]["frac"] == pytest.approx(1000.0 * b_frame / (bench.HBM_PEAK_GBS * 1e9), rel=1e-3)
+    # headline: BASELINE.md:44, fps x B_frame / peak
+    assert r["B_frame"] == b_frame
+    assert r["achieved"] == pytest.approx(1000.0 * b_frame / 1e9, rel=1e-3)
+    assert r["frac"] == pytest.approx(1000.0 * b_frame / (bench.HBM_PEAK_GBS * 1e9), rel=1e-3)
+    assert r["traffic"] == 99 and r["bound"] == "hbm" and r["unit"] == "GB/s" and r["avg_launch_ms"] == 2.0
+    own, whole, setup = r["kernels"]
+    assert own["kernel"] == whole["kernel"] == "k_raster" and setup["kernel"] == "k_setup"
+    assert own["bytes_per_launch"] == 10 * (200 + 300) * M
+    assert whole["bytes_per_launch"] == 10 * b_frame
+    assert whole["achieved"] == pytest.approx(10 * b_frame / 2e-3 / 1e9, rel=1e-3)
+    assert setup["bytes_per_launch"] == (1000 + 10 * 5 * bench.RECORD_BYTES) * M   # geometry once per launch
 
 
 def test_median_timing_runs_warmup_then_five():

@@ -60,7 +60,8 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
         here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         prof = {"workload": line["config"]["workload"].split(":")[0] if line else workload,
                 "frames_per_launch": line["config"]["frames_per_launch"] if line else frames_per_launch,
-                "B_frame": line["roofline"]["frame_level"]["B_frame"] if line else None,
+                "B_frame": (line["roofline"].get("B_frame") or line["roofline"].get("frame_level", {}).get("B_frame"))
+                if line else None,
                 "bytes_per_launch": {k: int(out[k]["hbm_bytes_per_launch"]) for k in ("k_raster", "k_setup")
                                      if "hbm_bytes_per_launch" in out.get(k, {})},
                 "k_raster_fetch_size_kb": out["k_raster"]["FETCH_SIZE"],
