@@ -17,7 +17,7 @@ KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
 COVERED_UNKNOWN = 0x80000000  # csg_outputs.label_covered flag: a tile held more than 32 labels
 ERR_CAPACITY = -6  # CSG_ERR_CAPACITY
 # csg_outputs.file_kinds (CSG_FILE_*): files encoded on the GPU, one per kind per frame, in bit order
-FILE_KINDS = {"rgb_png": 1, "depth_csv": 2, "depth_png": 4}
+FILE_KINDS = {"rgb_png": 1, "depth_csv": 2, "depth_png": 4, "pointcloud_txt": 8}
 
 EXPORTED = (
     "csg_create", "csg_destroy", "csg_last_error", "csg_abi_version", "csg_upload_scene",

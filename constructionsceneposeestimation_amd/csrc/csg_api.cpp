@@ -145,10 +145,11 @@ struct csg_ctx {
   // images of the last batch (for the file encoders) and the encoders' buffers
   const uint8_t* last_rgb = nullptr;
   const float* last_depth = nullptr;
+  const float* last_points = nullptr;
   const uint8_t* last_dvis = nullptr;
   DevBuf<EncPng> enc_rgb, enc_dpng;
   DevBuf<uint2> enc_rowsum;
-  DevBuf<uint32_t> enc_rows_rgb, enc_rows_dpng, enc_rows_csv;
+  DevBuf<uint32_t> enc_rows_rgb, enc_rows_dpng, enc_rows_csv, enc_rows_pcd;
   DevBuf<uint64_t> enc_fsize, enc_foff, enc_zoff;
   DevBuf<uint8_t> enc_zbuf, enc_out;
   DevBuf<uint8_t> dstat_part;           // depth-statistics partial sums
@@ -835,9 +836,13 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   if (!out->inst_stats) b.stats = nullptr;
   if (!out->label_covered || !out->n_labels) b.covered = nullptr;
   // images only a file needs go to internal scratch
-  if ((fk & CSG_FILE_RGB_PNG) && !b.rgb) {
+  if ((fk & (CSG_FILE_RGB_PNG | CSG_FILE_POINTCLOUD_TXT)) && !b.rgb) {
     HIP_TRY(c, c->o_rgb.alloc(F * npx * 3));
     b.rgb = c->o_rgb.p;
+  }
+  if ((fk & CSG_FILE_POINTCLOUD_TXT) && !b.points) {
+    HIP_TRY(c, c->o_points.alloc(F * npx * 3));
+    b.points = c->o_points.p;
   }
   if ((fk & CSG_FILE_DEPTH_CSV || out->depth_stats) && !b.depth) {
     HIP_TRY(c, c->o_depth.alloc(F * npx));
@@ -942,6 +947,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   HIP_TRY(c, hipGetLastError());
   c->last_rgb = b.rgb;
   c->last_depth = b.depth;
+  c->last_points = b.points;
   c->last_dvis = dvis;
   if (!dev) {
     if (out->rgb) HIP_TRY(c, hipMemcpyAsync(out->rgb, b.rgb, F * npx * 3, hipMemcpyDeviceToHost, st));
@@ -997,10 +1003,11 @@ static int copy_files(csg_ctx* c, uint8_t* dst, uint64_t cap, uint64_t* offsets)
 // synchronisation to size the buffers, then the bytes, then one D2H copy.
 static int encode_files(csg_ctx* c, const csg_outputs* out, uint32_t F) {
   const uint32_t fk = out->file_kinds;
-  uint32_t nk = 0, slot_rgb = 0, slot_csv = 0, slot_dpng = 0;
+  uint32_t nk = 0, slot_rgb = 0, slot_csv = 0, slot_dpng = 0, slot_pcd = 0;
   if (fk & CSG_FILE_RGB_PNG) slot_rgb = nk++;
   if (fk & CSG_FILE_DEPTH_CSV) slot_csv = nk++;
   if (fk & CSG_FILE_DEPTH_PNG) slot_dpng = nk++;
+  if (fk & CSG_FILE_POINTCLOUD_TXT) slot_pcd = nk++;
   const uint32_t W = c->cfg.width, H = c->cfg.height, n_files = F * nk;
   hipStream_t st = c->stream;
   const size_t rows = (size_t)F * png_units_per_frame(W, H), csv_rows = (size_t)F * csv_units_per_frame(W, H);
@@ -1023,6 +1030,10 @@ static int encode_files(csg_ctx* c, const csg_outputs* out, uint32_t F) {
   if (fk & CSG_FILE_DEPTH_CSV) {
     HIP_TRY(c, c->enc_rows_csv.alloc(csv_rows));
     launch_csv_sizes(c->last_depth, W, H, F, c->enc_rows_csv.p, c->enc_fsize.p, nk, slot_csv, st);
+  }
+  if (fk & CSG_FILE_POINTCLOUD_TXT) {
+    HIP_TRY(c, c->enc_rows_pcd.alloc(csv_rows));
+    launch_pcd_sizes(c->last_points, c->last_rgb, W, H, F, c->enc_rows_pcd.p, c->enc_fsize.p, nk, slot_pcd, st);
   }
   const EncPng* pa = (fk & CSG_FILE_RGB_PNG) ? c->enc_rgb.p : nullptr;
   const EncPng* pb = (fk & CSG_FILE_DEPTH_PNG) ? c->enc_dpng.p : nullptr;
@@ -1047,6 +1058,9 @@ static int encode_files(csg_ctx* c, const csg_outputs* out, uint32_t F) {
                     c->enc_foff.p, nk, slot_dpng, st);
   if (fk & CSG_FILE_DEPTH_CSV)
     launch_csv_emit(c->last_depth, W, H, F, c->enc_rows_csv.p, c->enc_out.p, c->enc_foff.p, nk, slot_csv, st);
+  if (fk & CSG_FILE_POINTCLOUD_TXT)
+    launch_pcd_emit(c->last_points, c->last_rgb, W, H, F, c->enc_rows_pcd.p, c->enc_out.p, c->enc_foff.p, nk, slot_pcd,
+                    st);
   HIP_TRY(c, hipGetLastError());
   c->enc_total = total;
   c->enc_nfiles = n_files;
@@ -1059,7 +1073,7 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
   // an earlier asynchronous batch that overflowed is reported, not lost
   int rc = csg_synchronize(c);
   if (rc) return rc;
-  if (out && (out->file_kinds & ~(CSG_FILE_RGB_PNG | CSG_FILE_DEPTH_CSV | CSG_FILE_DEPTH_PNG)))
+  if (out && (out->file_kinds & ~(CSG_FILE_RGB_PNG | CSG_FILE_DEPTH_CSV | CSG_FILE_DEPTH_PNG | CSG_FILE_POINTCLOUD_TXT)))
     return c->fail(CSG_ERR_INVALID, "render: unknown file kinds %#x", out->file_kinds);
   const uint32_t fk = out ? out->file_kinds : 0u;
   for (int attempt = 0; attempt < 6; ++attempt) {

@@ -269,33 +269,40 @@ CSG_HD uint32_t crc_entry(uint32_t k) {
 // ---------------------------------------------------------------------------
 constexpr int kMaxF6Chars = 48;
 
-CSG_HD int put_dec_u64(char* out, uint64_t v) {
-  char tmp[20];
-  int n = 0;
-  do {
-    tmp[n++] = (char)('0' + v % 10u);
-    v /= 10u;
-  } while (v);
-  for (int k = 0; k < n; ++k) out[k] = tmp[n - 1 - k];
-  return n;
-}
-
-CSG_HD int put_dec_u32(char* out, uint32_t v) {
-  char tmp[10];
-  int n = 0;
-  do {
-    tmp[n++] = (char)('0' + v % 10u);
-    v /= 10u;
-  } while (v);
-  for (int k = 0; k < n; ++k) out[k] = tmp[n - 1 - k];
-  return n;
-}
-
 CSG_HD int dec_digits_u32(uint32_t v) {
   int n = 1;
   while (v >= 10u) {
     v /= 10u;
     ++n;
+  }
+  return n;
+}
+
+CSG_HD int dec_digits_u64(uint64_t v) {
+  int n = 1;
+  while (v >= 10u) {
+    v /= 10u;
+    ++n;
+  }
+  return n;
+}
+
+// Digits written from the last one backwards straight into `out` (no local
+// array: on the GPU a dynamically indexed one lives in scratch memory).
+CSG_HD int put_dec_u64(char* out, uint64_t v) {
+  const int n = dec_digits_u64(v);
+  for (int k = n - 1; k >= 0; --k) {
+    out[k] = (char)('0' + v % 10u);
+    v /= 10u;
+  }
+  return n;
+}
+
+CSG_HD int put_dec_u32(char* out, uint32_t v) {
+  const int n = dec_digits_u32(v);
+  for (int k = n - 1; k >= 0; --k) {
+    out[k] = (char)('0' + v % 10u);
+    v /= 10u;
   }
   return n;
 }
@@ -402,14 +409,45 @@ CSG_HD int fmt6f_len(float x) {
   }
   const uint64_t q = scaled6(m, e);
   if (q < (1ull << 32)) return sign + dec_digits_u32((uint32_t)q / 1000000u) + 7;
-  uint64_t ip = q / 1000000u;
-  int n = 1;
-  while (ip >= 10u) {
-    ip /= 10u;
-    ++n;
-  }
-  return sign + n + 7;
+  return sign + dec_digits_u64(q / 1000000u) + 7;
 }
+
+// "%.6f" of an integer 0..255 (a point's colour channel as np.savetxt prints
+// it after np.hstack promotes it to float): its digits, then ".000000".
+CSG_HD int fmt6f_u8_len(uint32_t v) { return (v >= 100u ? 3 : v >= 10u ? 2 : 1) + 7; }
+CSG_HD int fmt6f_u8(uint32_t v, char* out) {
+  const int n = put_dec_u32(out, v);
+  out[n] = '.';
+  for (int d = 1; d <= 6; ++d) out[n + d] = '0';
+  return n + 7;
+}
+
+// One point-cloud line "x y z r g b\n" (np.savetxt(np.hstack([xyz, rgb]),
+// fmt="%.6f", delimiter=" "), GDP:766-770): its length, and its text.
+constexpr int kMaxPcdLine = 3 * kMaxF6Chars + 3 * 10 + 6;
+CSG_HD int pcd_line_len(float x, float y, float z, uint32_t r, uint32_t g, uint32_t b) {
+  return fmt6f_len(x) + fmt6f_len(y) + fmt6f_len(z) + fmt6f_u8_len(r) + fmt6f_u8_len(g) + fmt6f_u8_len(b) + 6;
+}
+CSG_HD int pcd_line(float x, float y, float z, uint32_t r, uint32_t g, uint32_t b, char* out) {
+  int p = fmt6f(x, out);
+  out[p++] = ' ';
+  p += fmt6f(y, out + p);
+  out[p++] = ' ';
+  p += fmt6f(z, out + p);
+  out[p++] = ' ';
+  p += fmt6f_u8(r, out + p);
+  out[p++] = ' ';
+  p += fmt6f_u8(g, out + p);
+  out[p++] = ' ';
+  p += fmt6f_u8(b, out + p);
+  out[p++] = '\n';
+  return p;
+}
+// The file's first line (header="x y z r g b", comments="").
+constexpr uint32_t kPcdHeaderBytes = 12;
+CSG_HD char pcd_header_byte(uint32_t k) { return "x y z r g b\n"[k]; }
+// A pixel is a point when its world position is a number (NaN: nothing hit).
+CSG_HD bool pcd_valid(float x, float y, float z) { return x == x && y == y && z == z; }
 
 }  // namespace dfl
 }  // namespace csg

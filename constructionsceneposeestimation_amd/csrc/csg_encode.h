@@ -35,6 +35,11 @@ void launch_png_emit(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, con
                      uint32_t kslot, hipStream_t st);
 void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,
                      const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st);
+// Point-cloud TXT: units as the CSV's (64 pixels of a row); points [F][H][W][3] f32, rgb [F][H][W][3].
+void launch_pcd_sizes(const float* points, const uint8_t* rgb, uint32_t W, uint32_t H, uint32_t F, uint32_t* rowlen,
+                      uint64_t* fsize, uint32_t nk, uint32_t kslot, hipStream_t st);
+void launch_pcd_emit(const float* points, const uint8_t* rgb, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff,
+                     uint8_t* out, const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st);
 
 // Quality-log depth statistics of F frames: out [F][6] (csg_outputs.depth_stats);
 // scratch of depth_stats_scratch_bytes(F).

@@ -337,19 +337,91 @@ __global__ __launch_bounds__(256) void k_png_layout(EncPng* __restrict__ png, ui
 }
 
 // ---------------------------------------------------------------------------
-// CSV passes
+// Text files (depth CSV, point-cloud TXT): one wave per unit of 64 items
 // ---------------------------------------------------------------------------
-// Unit u of a frame: row u / V, values [(u % V) * kSegVals, ...), each followed
-// by a space, the row's last by a newline.
-__global__ __launch_bounds__(kRowsPerBlock) void k_csv_len(const float* __restrict__ depth, uint32_t W, uint32_t H,
-                                                           uint32_t* __restrict__ ulen) {
-  const uint32_t f = blockIdx.y, V = csv_units(W), u = blockIdx.x * kRowsPerBlock + threadIdx.x;
+// A unit is 64 consecutive pixels of one row (the row's last unit may be
+// short); lane i owns pixel i.  The length pass reduces the lanes' text
+// lengths to the unit's; the emit pass scans them, each lane formats its text
+// into the wave's LDS buffer at its offset, and the wave copies the buffer to
+// the file with coalesced dword stores (the unaligned ends as bytes).  A unit
+// whose text does not fit the buffer (values past ~1e30) writes lane by lane.
+constexpr uint32_t kTxtWaves = 4;          // units per 256-thread workgroup
+constexpr uint32_t kTxtBuf = 6144;         // LDS bytes per wave (64 typical point lines need ~4 KB)
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t& total) {
+  uint32_t s = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(s, o, 64);
+    if (lane >= (uint32_t)o) s += t;
+  }
+  total = __shfl(s, 63, 64);
+  return s - v;
+}
+
+// Copy n bytes of the wave's LDS text to out + pos: head and tail bytes with
+// byte stores (those dwords are shared with the neighbouring units), the
+// dwords between with one coalesced store per lane and round.
+__device__ __forceinline__ void wave_copy_out(const uint32_t* buf, uint32_t n, uint8_t* out, uint64_t pos,
+                                              uint32_t lane) {
+  const uint8_t* bb = reinterpret_cast<const uint8_t*>(buf);
+  const uint64_t end = pos + n, a0 = min((pos + 3u) & ~3ull, end), a1 = max(end & ~3ull, a0);
+  const uint32_t head = (uint32_t)(a0 - pos), tail = (uint32_t)(end - a1);
+  if (lane < head) out[pos + lane] = bb[lane];
+  if (lane < tail) out[a1 + lane] = bb[(uint32_t)(a1 - pos) + lane];
+  const uint32_t nw = (uint32_t)((a1 - a0) >> 2);
+  uint32_t* ow = reinterpret_cast<uint32_t*>(out + a0);
+  for (uint32_t j = lane; j < nw; j += 64u) {
+    const uint32_t o = head + 4u * j, w = o >> 2, sh = o & 3u;
+    const uint32_t lo = buf[w], hi = buf[w + 1];
+    ow[j] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+  }
+}
+
+// Unit u of a frame: row u / V, pixels [(u % V) * 64, ...) of it.
+__device__ __forceinline__ void txt_unit(uint32_t u, uint32_t V, uint32_t W, uint32_t& r, uint32_t& x0, uint32_t& x1) {
+  r = u / V;
+  x0 = (u - r * V) * kSegVals;
+  x1 = min(x0 + kSegVals, W);
+}
+
+// Depth CSV: each value followed by a space, the row's last by a newline.
+__global__ __launch_bounds__(64 * kTxtWaves) void k_csv_len(const float* __restrict__ depth, uint32_t W, uint32_t H,
+                                                            uint32_t* __restrict__ ulen) {
+  const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u;
+  const uint32_t u = blockIdx.x * kTxtWaves + (threadIdx.x >> 6);
   if (u >= H * V) return;
-  const uint32_t r = u / V, x0 = (u - r * V) * kSegVals, x1 = min(x0 + kSegVals, W);
-  const float* row = depth + ((size_t)f * H + r) * W;
-  uint32_t n = x1 - x0;   // separators
-  for (uint32_t x = x0; x < x1; ++x) n += (uint32_t)fmt6f_len(row[x]);
-  ulen[(size_t)f * H * V + u] = n;
+  uint32_t r, x0, x1;
+  txt_unit(u, V, W, r, x0, x1);
+  const uint32_t x = x0 + lane;
+  const uint32_t n = x < x1 ? (uint32_t)fmt6f_len(depth[((size_t)f * H + r) * W + x]) + 1u : 0u;
+  const uint32_t tot = wave_sum(n);
+  if (lane == 0) ulen[(size_t)f * H * V + u] = tot;
+}
+
+// Point-cloud TXT: one line per pixel with a point, in row-major order; the
+// frame's unit 0 also carries the 12-byte header line.
+__global__ __launch_bounds__(64 * kTxtWaves) void k_pcd_len(const float* __restrict__ pts, const uint8_t* __restrict__ rgb,
+                                                            uint32_t W, uint32_t H, uint32_t* __restrict__ ulen) {
+  const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u;
+  const uint32_t u = blockIdx.x * kTxtWaves + (threadIdx.x >> 6);
+  if (u >= H * V) return;
+  uint32_t r, x0, x1;
+  txt_unit(u, V, W, r, x0, x1);
+  const uint32_t x = x0 + lane;
+  uint32_t n = 0;
+  if (x < x1) {
+    const size_t px = ((size_t)f * H + r) * W + x;
+    const float X = pts[3 * px], Y = pts[3 * px + 1], Z = pts[3 * px + 2];
+    if (pcd_valid(X, Y, Z)) n = (uint32_t)pcd_line_len(X, Y, Z, rgb[3 * px], rgb[3 * px + 1], rgb[3 * px + 2]);
+  }
+  const uint32_t tot = wave_sum(n);
+  if (lane == 0) ulen[(size_t)f * H * V + u] = tot + (u == 0 ? kPcdHeaderBytes : 0u);
 }
 
 __global__ __launch_bounds__(256) void k_csv_layout(uint32_t* __restrict__ ulen, uint32_t n, uint64_t* __restrict__ fsize,
@@ -580,23 +652,95 @@ __global__ __launch_bounds__(64) void k_png_pack(const EncPng* __restrict__ png,
   o.finish();
 }
 
-__global__ __launch_bounds__(kRowsPerBlock) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
-                                                            const uint32_t* __restrict__ uoff, uint8_t* out,
-                                                            const uint64_t* __restrict__ foff, uint32_t nk,
-                                                            uint32_t kslot) {
-  const uint32_t f = blockIdx.y, V = csv_units(W), u = blockIdx.x * kRowsPerBlock + threadIdx.x;
-  if (u >= H * V) return;
-  const uint32_t r = u / V, x0 = (u - r * V) * kSegVals, x1 = min(x0 + kSegVals, W);
-  const float* row = depth + ((size_t)f * H + r) * W;
+// A lane's text written straight to the file when the unit overflows the LDS buffer.
+__device__ __noinline__ void put_text_direct(uint8_t* out, uint64_t pos, const char* s, int n) {
   ByteOut o;
-  o.init(out, foff[(size_t)f * nk + kslot] + uoff[(size_t)f * H * V + u]);
-  char tmp[kMaxF6Chars];
-  for (uint32_t x = x0; x < x1; ++x) {
-    const int n = fmt6f(row[x], tmp);
-    for (int k = 0; k < n; ++k) o.put((uint8_t)tmp[k]);
-    o.put(x + 1u < W ? ' ' : '\n');
-  }
+  o.init(out, pos);
+  for (int k = 0; k < n; ++k) o.put((uint8_t)s[k]);
   o.finish();
+}
+
+__global__ __launch_bounds__(64 * kTxtWaves) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
+                                                             const uint32_t* __restrict__ uoff, uint8_t* out,
+                                                             const uint64_t* __restrict__ foff, uint32_t nk,
+                                                             uint32_t kslot) {
+  __shared__ uint32_t tbuf[kTxtWaves][kTxtBuf / 4 + 1];
+  const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t u = blockIdx.x * kTxtWaves + wv;
+  if (u >= H * V) return;
+  uint32_t r, x0, x1;
+  txt_unit(u, V, W, r, x0, x1);
+  const uint32_t x = x0 + lane;
+  const float d = x < x1 ? depth[((size_t)f * H + r) * W + x] : 0.0f;
+  const uint32_t n = x < x1 ? (uint32_t)fmt6f_len(d) + 1u : 0u;
+  uint32_t total;
+  const uint32_t off = wave_excl_scan(n, lane, total);
+  const uint64_t pos = foff[(size_t)f * nk + kslot] + uoff[(size_t)f * H * V + u];
+  const char sep = x + 1u < W ? ' ' : '\n';
+  if (total > kTxtBuf) {
+    if (n) {
+      char tmp[kMaxF6Chars + 1];
+      const int k = fmt6f(d, tmp);
+      tmp[k] = sep;
+      put_text_direct(out, pos + off, tmp, k + 1);
+    }
+    return;
+  }
+  char* t = reinterpret_cast<char*>(tbuf[wv]);
+  if (n) {
+    fmt6f(d, t + off);
+    t[off + n - 1u] = sep;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_copy_out(tbuf[wv], total, out, pos, lane);
+}
+
+__global__ __launch_bounds__(64 * kTxtWaves) void k_pcd_emit(const float* __restrict__ pts, const uint8_t* __restrict__ rgb,
+                                                             uint32_t W, uint32_t H, const uint32_t* __restrict__ uoff,
+                                                             uint8_t* out, const uint64_t* __restrict__ foff,
+                                                             uint32_t nk, uint32_t kslot) {
+  __shared__ uint32_t tbuf[kTxtWaves][kTxtBuf / 4 + 1];
+  const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t u = blockIdx.x * kTxtWaves + wv;
+  if (u >= H * V) return;
+  uint32_t r, x0, x1;
+  txt_unit(u, V, W, r, x0, x1);
+  const uint32_t x = x0 + lane;
+  float X = 0.0f, Y = 0.0f, Z = 0.0f;
+  uint32_t R = 0, G = 0, B = 0, n = 0;
+  if (x < x1) {
+    const size_t px = ((size_t)f * H + r) * W + x;
+    X = pts[3 * px];
+    Y = pts[3 * px + 1];
+    Z = pts[3 * px + 2];
+    R = rgb[3 * px];
+    G = rgb[3 * px + 1];
+    B = rgb[3 * px + 2];
+    if (pcd_valid(X, Y, Z)) n = (uint32_t)pcd_line_len(X, Y, Z, R, G, B);
+  }
+  const uint32_t hdr = u == 0 ? kPcdHeaderBytes : 0u;
+  uint32_t total;
+  const uint32_t off = wave_excl_scan(n, lane, total) + hdr;
+  total += hdr;
+  const uint64_t pos = foff[(size_t)f * nk + kslot] + uoff[(size_t)f * H * V + u];
+  if (total > kTxtBuf) {
+    if (lane < hdr) out[pos + lane] = (uint8_t)pcd_header_byte(lane);
+    if (n) {
+      char tmp[kMaxPcdLine];
+      const int k = pcd_line(X, Y, Z, R, G, B, tmp);
+      put_text_direct(out, pos + off, tmp, k);
+    }
+    return;
+  }
+  char* t = reinterpret_cast<char*>(tbuf[wv]);
+  if (lane < hdr) t[lane] = pcd_header_byte(lane);
+  if (n) pcd_line(X, Y, Z, R, G, B, t + off);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_copy_out(tbuf[wv], total, out, pos, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -689,8 +833,16 @@ void launch_png_sizes(const uint8_t* img, uint32_t W, uint32_t H, uint32_t F, En
 void launch_csv_sizes(const float* depth, uint32_t W, uint32_t H, uint32_t F, uint32_t* ulen, uint64_t* fsize,
                       uint32_t nk, uint32_t kslot, hipStream_t st) {
   const uint32_t n = csv_units_per_frame(W, H);
-  const dim3 units((n + kRowsPerBlock - 1) / kRowsPerBlock, F);
-  hipLaunchKernelGGL(k_csv_len, units, dim3(kRowsPerBlock), 0, st, depth, W, H, ulen);
+  const dim3 units((n + kTxtWaves - 1) / kTxtWaves, F);
+  hipLaunchKernelGGL(k_csv_len, units, dim3(64 * kTxtWaves), 0, st, depth, W, H, ulen);
+  hipLaunchKernelGGL(k_csv_layout, dim3(F), dim3(256), 0, st, ulen, n, fsize, nk, kslot);
+}
+
+void launch_pcd_sizes(const float* points, const uint8_t* rgb, uint32_t W, uint32_t H, uint32_t F, uint32_t* ulen,
+                      uint64_t* fsize, uint32_t nk, uint32_t kslot, hipStream_t st) {
+  const uint32_t n = csv_units_per_frame(W, H);
+  const dim3 units((n + kTxtWaves - 1) / kTxtWaves, F);
+  hipLaunchKernelGGL(k_pcd_len, units, dim3(64 * kTxtWaves), 0, st, points, rgb, W, H, ulen);
   hipLaunchKernelGGL(k_csv_layout, dim3(F), dim3(256), 0, st, ulen, n, fsize, nk, kslot);
 }
 
@@ -724,7 +876,14 @@ void launch_depth_stats(const float* depth, uint32_t npx, uint32_t F, void* scra
 void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,
                      const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
   const uint32_t n = csv_units_per_frame(W, H);
-  hipLaunchKernelGGL(k_csv_emit, dim3((n + kRowsPerBlock - 1) / kRowsPerBlock, F), dim3(kRowsPerBlock), 0, st, depth,
+  hipLaunchKernelGGL(k_csv_emit, dim3((n + kTxtWaves - 1) / kTxtWaves, F), dim3(64 * kTxtWaves), 0, st, depth, W, H,
+                     rowoff, out, foff, nk, kslot);
+}
+
+void launch_pcd_emit(const float* points, const uint8_t* rgb, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff,
+                     uint8_t* out, const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
+  const uint32_t n = csv_units_per_frame(W, H);
+  hipLaunchKernelGGL(k_pcd_emit, dim3((n + kTxtWaves - 1) / kTxtWaves, F), dim3(64 * kTxtWaves), 0, st, points, rgb,
                      W, H, rowoff, out, foff, nk, kslot);
 }
 

@@ -311,7 +311,8 @@ int csgio_write_label_json(const char* path, const csgio_label* L) {
     const int32_t lab = L->obj_label[j];
     if (lab < 0 || (uint32_t)lab >= L->n_labels) continue;
     const uint32_t* st = L->inst_stats + (size_t)lab * 5;
-    if (st[0] == 0) continue;
+    const bool hidden = st[0] == 0;
+    if (hidden && !(L->obj_listed && L->obj_listed[j])) continue;
     o += n_vis++ ? ",\n    {\n" : "[\n    {\n";
     o += L->obj_head[j];
     o += ",\n      \"pixel_count\": ";
@@ -319,13 +320,15 @@ int csgio_write_label_json(const char* path, const csgio_label* L) {
     o += ",\n      \"bbox_2d\": [";
     for (int k = 1; k < 5; ++k) {
       o += k > 1 ? ",\n        " : "\n        ";
-      put_int(st[k]);
+      put_int(hidden ? -1 : (long long)st[k]);
     }
     o += "\n      ]";
     if (L->covered) {   // occlusionRatio: 1 - visible / covered, float32 (labels.occlusion_ratios); -1 unknown
       const uint32_t cv = L->covered[lab];
       const uint32_t cnt = cv & 0x7FFFFFFFu;
-      const float occ = (!(cv & 0x80000000u) && cnt) ? (float)(1.0 - (double)st[0] / (double)cnt) : -1.0f;
+      const bool known = !(cv & 0x80000000u);
+      const float occ = hidden ? (known ? 1.0f : -1.0f)
+                               : (known && cnt) ? (float)(1.0 - (double)st[0] / (double)cnt) : -1.0f;
       o += ",\n      \"occlusion_ratio\": ";
       put_dbl((double)occ);
     }

@@ -15,13 +15,13 @@ same files:
   depth/depth_%06d.csv             (:1687-1688)
   depth/depth_%06d.png             (:1690-1709, JET colour map made on the GPU)
   depth/depth_%06d.npy             (optional)
-  pointcloud/pointcloud_%06d.txt   (:1716-1724, optional; points from the GPU resolve)
+  pointcloud/pointcloud_%06d.txt   (:1716-1757; points from the GPU resolve, text encoded on the GPU)
   normals/normals_%06d.npy         (C5 normals, f16, optional)
   logs/generation_summary.json     (:2090; statistics, frame_logs, counters)
   logs/generation_detail.log       (:254-263, per-frame entries + report)
 
-The default outputs are the reference's (RGB PNG, depth CSV + PNG, mask
-.npy, label JSON); ``--outputs`` picks others.
+The default outputs are the reference's (RGB PNG, depth CSV + PNG, point
+cloud TXT, mask .npy, label JSON); ``--outputs`` picks others.
 
 Sharding: ``--rank/--world`` (or RANK/WORLD_SIZE) pick the epochs this
 process owns (shard.shard_of_range); no communication between shards.
@@ -43,7 +43,7 @@ from typing import List, Optional
 import numpy as np
 
 from . import camera_math as cm
-from .labels import label_record, object_poses
+from .labels import OBJECT_LISTS, in_frustum, label_record, object_poses
 from .quality_log import QualityLog
 from .renderer import Renderer, make_frames, output_spec, scene_labels
 from .shard import shard_of_range
@@ -70,9 +70,23 @@ def _log_done(log: QualityLog, fut, log_args: dict, points: bool) -> None:
 
 
 OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png", "depth_npy", "pointcloud", "normals")
-# What the reference writes for every frame (GDP:1668-1711, 2055-2072): RGB PNG, depth CSV and
-# JET depth PNG, instance mask .npy; the label JSON is always written (it is the resume marker).
-REFERENCE_OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png")
+# What the reference writes for every frame (GDP:1668-1771, 2055-2072): RGB PNG, depth CSV and
+# JET depth PNG, point-cloud TXT, instance mask .npy; the label JSON is always written (it is the
+# resume marker).
+REFERENCE_OUTPUTS = ("rgb", "mask", "depth_csv", "depth_png", "pointcloud")
+
+
+# outputs encoded on the GPU in thread mode -> their csg_outputs.file_kinds kind (_lib.FILE_KINDS)
+FILE_OF_OUTPUT = (("rgb", "rgb_png"), ("depth_csv", "depth_csv"), ("depth_png", "depth_png"),
+                  ("pointcloud", "pointcloud_txt"))
+_PATHS = {"rgb": ("rgb", "rgb_{:06d}.png"), "depth_csv": ("depth", "depth_{:06d}.csv"),
+          "depth_png": ("depth", "depth_{:06d}.png"), "pointcloud": ("pointcloud", "pointcloud_{:06d}.txt")}
+
+
+def file_path(out_dir: str, output: str, frame: int) -> str:
+    """The reference's file name of one output of a frame (GDP:1668-1716)."""
+    d, name = _PATHS[output]
+    return os.path.join(out_dir, d, name.format(frame))
 
 
 def parse_outputs(spec: str) -> tuple:
@@ -91,14 +105,20 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
              resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
-             writer_mode: str = "thread", renderers: int = 0) -> dict:
+             writer_mode: str = "thread", renderers: int = 0, object_list: str = "visible") -> dict:
     """Render ``frames`` on one GPU and write them (``outputs``, default the
     reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
     add the depth .npy, the depth .npy + CSV, the point cloud, the normals).
     ``writer_mode`` "thread" encodes in threads of this process (the native
     writers release the GIL), "process" in worker processes fed through
     shared memory (writer_pool.py; measured slower at 1080p C3: 184 vs 233
-    frames/s, page faults on the shared ring and task pickling)."""
+    frames/s, page faults on the shared ring and task pickling).
+    ``object_list``: "visible" lists the objects with visible pixels in each
+    label file; "frustum" also those whose 3D box meets the view frustum
+    (labels.label_record; the reference lists Replicator's bounding_box_3d
+    primPaths, whose inclusion rule is closed)."""
+    if object_list not in OBJECT_LISTS:
+        raise ValueError(f"object_list {object_list!r}: choose from {OBJECT_LISTS}")
     outs = set(REFERENCE_OUTPUTS if outputs is None else outputs)
     if depth or depth_csv:
         outs.add("depth_npy")
@@ -113,20 +133,19 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         os.makedirs(os.path.join(out_dir, d), exist_ok=True)
     if resume:
         frames = [f for f in frames if not os.path.exists(os.path.join(out_dir, "labels", f"label_{f:06d}.json"))]
-    # Thread writers (the default): the PNGs and the depth CSV are encoded on
-    # the GPU (Renderer.render_files, csg_encode.hip) and the host only writes
-    # bytes; writer processes encode on the host (libcsgio).
+    # Thread writers (the default): the PNGs, the depth CSV and the point
+    # cloud are encoded on the GPU (Renderer.render_files, csg_encode.hip) and
+    # the host only writes bytes; writer processes encode on the host (libcsgio).
     gpu_files = writer_mode == "thread"
-    kinds = tuple(k for o, k in (("rgb", "rgb_png"), ("depth_csv", "depth_csv"), ("depth_png", "depth_png"))
-                  if o in outs) if gpu_files else ()
+    kinds = tuple(k for o, k in FILE_OF_OUTPUT if o in outs) if gpu_files else ()
     # host depth for its own files; the quality log's depth counts come from
     # the GPU (depth_stats) in thread mode, from the host depth otherwise
-    host_depth = bool(outs & {"depth_npy", "pointcloud"}) or (not gpu_files and "depth_csv" in outs)
+    host_depth = "depth_npy" in outs or (not gpu_files and bool(outs & {"depth_csv", "pointcloud"}))
     log = QualityLog(os.path.join(out_dir, "logs"))
     if gpu_files:
         want = (["keypoints", "stats", "covered", "depth_stats"] + (["instance"] if "mask" in outs else [])
                 + (["depth"] if host_depth else []) + (["depth_range"] if "depth_png" in outs else [])
-                + (["points", "rgb"] if "pointcloud" in outs else []) + (["normals"] if "normals" in outs else []))
+                + (["normals"] if "normals" in outs else []))
     else:
         want = (["rgb", "instance", "keypoints", "stats", "covered"] + (["depth"] if host_depth else [])
                 + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
@@ -144,8 +163,9 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     r = rends[0]
     if gpu_files:   # page-locked slots, and buffers for the encoded files (an estimate, grown on demand)
         npx = wl.width * wl.height
-        est = {"rgb_png": 2 * npx, "depth_csv": 10 * npx, "depth_png": npx}
-        pool.use_pinned(r.host_buffer, batch * sum(est[k] for k in kinds) + (1 << 20) if kinds else 0)
+        est = {"rgb_png": 2 * npx, "depth_csv": 10 * npx, "depth_png": npx, "pointcloud_txt": 48 * npx}
+        pool.use_pinned(r.host_buffer, batch * sum(est[k] for k in kinds) + (1 << 20) if kinds else 0,
+                        free=r.free_host_buffer)
     nk = len(kinds)
     intr = wl.intr
     # thread mode: label files written natively from the frame's arrays (no GIL)
@@ -231,16 +251,19 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                     pose_cache[e] = object_poses(wl.scene, wl.epoch(e).object_frames)
             for k, f in enumerate(fb):
                 V, P, C, cam, aim, q = wl.camera(f)
+                listed = (in_frustum(wl.scene, wl.epoch(f // 10).object_frames, V, P, wl.width, wl.height,
+                                     intr.near, intr.far) if object_list == "frustum" else None)
                 if lw is not None:
                     ep = lw.epoch(f // 10, pose_cache[f // 10])
                     lab = partial(lw.write, frame_id=f, camera_pose=cm.get_obj_pose_from_matrix(C), ep=ep,
                                   inst_stats=out["inst_stats"][k], covered=out["label_covered"][k],
-                                  kp_uv=out["keypoints_uv"][k], kp_vis=out["keypoints_vis"][k])
-                    n_obj = lw.n_visible(ep, out["inst_stats"][k])
+                                  kp_uv=out["keypoints_uv"][k], kp_vis=out["keypoints_vis"][k], listed=listed)
+                    n_obj = lw.n_visible(ep, out["inst_stats"][k], listed)
                 else:
                     lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
                                        out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
-                                       wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k])
+                                       wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k],
+                                       listed=listed)
                     n_obj = lab["num_objects"]
                 log_args = dict(n_objects=n_obj, kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
                                 cam_pos=cam, depth_range=out["depth_range"][k].copy() if "depth_range" in out else None)
@@ -251,24 +274,21 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                                                    "max": v[5]}
                 files = []
                 if kinds:   # GPU-encoded: file j = frame * nk + index of its kind
-                    for o, kd, path in (("rgb", "rgb_png", os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png")),
-                                        ("depth_csv", "depth_csv", os.path.join(out_dir, "depth", f"depth_{f:06d}.csv")),
-                                        ("depth_png", "depth_png", os.path.join(out_dir, "depth", f"depth_{f:06d}.png"))):
+                    for o, kd in FILE_OF_OUTPUT:
                         if o in outs:
-                            files.append((path, "encoded", (k * nk + kinds.index(kd),)))
+                            files.append((file_path(out_dir, o, f), "encoded", (k * nk + kinds.index(kd),)))
                 elif "rgb" in outs:
-                    files.append((os.path.join(out_dir, "rgb", f"rgb_{f:06d}.png"), "png", ("rgb",)))
+                    files.append((file_path(out_dir, "rgb", f), "png", ("rgb",)))
                 if "mask" in outs:
                     files.append((os.path.join(out_dir, "labels", f"instance_mask_{f:06d}.npy"), "npy", ("instance",)))
                 if "depth_npy" in outs:
                     files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.npy"), "npy", ("depth",)))
                 if "depth_csv" in outs and not kinds:
-                    files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.csv"), "csv", ("depth",)))
+                    files.append((file_path(out_dir, "depth_csv", f), "csv", ("depth",)))
                 if "depth_png" in outs and not kinds:
-                    files.append((os.path.join(out_dir, "depth", f"depth_{f:06d}.png"), "png", ("depth_vis",)))
-                if "pointcloud" in outs:
-                    files.append((os.path.join(out_dir, "pointcloud", f"pointcloud_{f:06d}.txt"), "pointcloud",
-                                  ("points", "rgb")))
+                    files.append((file_path(out_dir, "depth_png", f), "png", ("depth_vis",)))
+                if "pointcloud" in outs and not kinds:
+                    files.append((file_path(out_dir, "pointcloud", f), "pointcloud", ("points", "rgb")))
                 if "normals" in outs:
                     files.append((os.path.join(out_dir, "normals", f"normals_{f:06d}.npy"), "npy", ("normals",)))
                 fut = pool.submit(slot, k, files, lab, os.path.join(out_dir, "labels", f"label_{f:06d}.json"))
@@ -321,13 +341,16 @@ def main(argv=None):
     ap.add_argument("--writer-mode", default="thread", choices=("thread", "process"))
     ap.add_argument("--renderers", type=int, default=0,
                     help="renderer contexts rendering alternate batches (0: 2 with writer threads, else 1)")
+    ap.add_argument("--object-list", default="visible", choices=OBJECT_LISTS,
+                    help="objects in each label file: with visible pixels, or also every one in the view frustum")
     ap.add_argument("--no-resume", action="store_true")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
                        a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
-                       outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode, renderers=a.renderers)
+                       outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode, renderers=a.renderers,
+                       object_list=a.object_list)
     print(json.dumps(summary))
 
 

@@ -101,13 +101,55 @@ def object_poses(scene, object_frames) -> List[dict]:
             for o, c, sz, e in zip(scene.objects, center.tolist(), size.tolist(), euler.tolist())]
 
 
+OBJECT_LISTS = ("visible", "frustum")
+
+
+def in_frustum(scene, object_frames: Sequence[np.ndarray], view: np.ndarray, proj: np.ndarray, width: int,
+               height: int, near: float, far: float) -> np.ndarray:
+    """Per object of ``scene.objects``: does its 3D box (local bounds under
+    its object frame, the bounding_box_3d record) meet the view frustum?  A
+    box is outside when all 8 corners fail the same clip plane (W < near,
+    W > far, u < 0, u > width, v < 0, v > height in the pixel projection's
+    homogeneous rows 0, 1, 3); otherwise it counts as inside (conservative).
+    Objects without bounds are tested as the point at their origin."""
+    n = len(scene.objects)
+    out = np.zeros(n, bool)
+    if n == 0:
+        return out
+    lo = np.zeros((n, 3))
+    hi = np.zeros((n, 3))
+    for j, o in enumerate(scene.objects):
+        if o.local_bounds is not None:
+            lo[j], hi[j] = o.local_bounds
+    sel = np.array([[(c >> 0) & 1, (c >> 1) & 1, (c >> 2) & 1] for c in range(8)], np.float64)
+    corners = lo[:, None, :] + sel[None] * (hi - lo)[:, None, :]                  # [n][8][3]
+    M = np.asarray(object_frames, np.float64).reshape(n, 4, 4)
+    world = np.einsum("nij,nkj->nki", M[:, :3, :3], corners) + M[:, None, :3, 3]
+    PV = np.asarray(proj, np.float64).reshape(4, 4) @ np.asarray(view, np.float64).reshape(4, 4)
+    clip = np.einsum("ij,nkj->nki", PV, np.concatenate([world, np.ones((n, 8, 1))], 2))
+    X, Y, Wc = clip[..., 0], clip[..., 1], clip[..., 3]
+    outside = ((Wc < near).all(1) | (Wc > far).all(1) | (X < 0).all(1) | (X > width * Wc).all(1)
+               | (Y < 0).all(1) | (Y > height * Wc).all(1))
+    return ~outside
+
+
 def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dict, poses: List[dict],
                  inst_stats: Optional[np.ndarray], kp_uv: Optional[np.ndarray], kp_vis: Optional[np.ndarray],
                  kp_table: Optional[Sequence], height: int, width: int,
-                 covered: Optional[np.ndarray] = None) -> dict:
+                 covered: Optional[np.ndarray] = None, listed: Optional[Sequence[bool]] = None) -> dict:
     """The label JSON of one frame (:2056-2064) for the objects visible in it
-    (+ ``occlusion_ratio`` per object when the coverage is given)."""
+    (+ ``occlusion_ratio`` per object when the coverage is given).
+
+    Which objects are listed.  The reference lists the ``bounding_box_3d``
+    annotator's primPaths (GDP:1780-1906); Replicator's inclusion rule for
+    that list is closed.  By default ("visible") this build lists the objects
+    with at least one visible pixel.  With ``listed`` (per object of
+    ``poses``: e.g. :func:`in_frustum`, the "frustum" object list) those
+    objects are listed too when no pixel of them is visible: pixel_count 0,
+    bbox_2d [-1, -1, -1, -1] and occlusion_ratio 1.0 (-1.0 when the coverage
+    is unknown)."""
     occ = occlusion_ratios(inst_stats[:, 0], covered) if inst_stats is not None and covered is not None else None
+    cov_known = ((np.asarray(covered, np.uint32) & COVERED_UNKNOWN) == 0).tolist() if occ is not None else None
     occ = occ.tolist() if occ is not None else None
     objs = []
     kp_by_obj: Dict[int, list] = {}
@@ -118,16 +160,20 @@ def label_record(frame_id: int, camera_pose: Sequence[float], camera_params: dic
     stats = inst_stats.tolist() if inst_stats is not None else None
     for j, p in enumerate(poses):
         i = p["inst_idx"]
+        hidden = False
         if stats is not None:
-            if i >= len(stats) or stats[i][0] == 0:
+            if i >= len(stats):
+                continue
+            hidden = stats[i][0] == 0
+            if hidden and not (listed is not None and listed[j]):
                 continue
         e = dict(p)
         if stats is not None:
             st = stats[i]
             e["pixel_count"] = st[0]
-            e["bbox_2d"] = st[1:5]
+            e["bbox_2d"] = [-1, -1, -1, -1] if hidden else st[1:5]
             if occ is not None:
-                e["occlusion_ratio"] = occ[i]
+                e["occlusion_ratio"] = (1.0 if cov_known[i] else -1.0) if hidden else occ[i]
         if j in kp_by_obj:
             e["keypoints_2d"] = kp_by_obj[j]
         objs.append(e)

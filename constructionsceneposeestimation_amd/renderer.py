@@ -241,10 +241,21 @@ class Renderer:
         self._pinned.append(p)
         return arr
 
+    def free_host_buffer(self, arr: np.ndarray) -> None:
+        """Release a :meth:`host_buffer` array now (instead of with the
+        renderer); the caller guarantees nothing reads it any more."""
+        addr = arr.ctypes.data
+        for k, p in enumerate(self._pinned):
+            if p.value == addr:
+                self._check(self.lib.csg_host_free(self.ctx, p), "host_free")
+                del self._pinned[k]
+                return
+        raise CsgError("free_host_buffer: not a buffer of this renderer")
+
     def render_files(self, frames: np.ndarray, kinds: Sequence[str], files: np.ndarray,
                      want: Iterable[str] = (), out: Optional[Dict[str, np.ndarray]] = None):
         """Render a batch (at most ``max_frames``) and encode ``kinds`` (of
-        ``_lib.FILE_KINDS``: "rgb_png", "depth_csv", "depth_png") on the GPU
+        ``_lib.FILE_KINDS``: "rgb_png", "depth_csv", "depth_png", "pointcloud_txt") on the GPU
         into ``files`` (uint8 host array, pinned from :meth:`host_buffer` for
         speed), growing nothing: returns (outputs dict as :meth:`render`,
         offsets) with file j = frame * len(kinds) + k (kinds in bit order) at

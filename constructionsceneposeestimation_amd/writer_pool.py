@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import multiprocessing as mp
 import os
+import threading
 from concurrent.futures import Future, ProcessPoolExecutor, ThreadPoolExecutor
 from typing import Dict, List, Optional, Tuple
 
@@ -152,12 +153,15 @@ class WriterPool:
         else:
             raise ValueError(f"writer mode {mode!r}: 'process' or 'thread'")
 
-    def use_pinned(self, alloc, files_bytes: int = 0) -> None:
+    def use_pinned(self, alloc, files_bytes: int = 0, free=None) -> None:
         """Thread mode: the slots' arrays in page-locked memory from
         ``alloc(nbytes)`` (Renderer.host_buffer: device-to-host copies at full
         PCIe rate), plus a ``files`` buffer of ``files_bytes`` per slot for the
-        files the GPU encodes (Renderer.render_files)."""
+        files the GPU encodes (Renderer.render_files); ``free(array)``
+        (Renderer.free_host_buffer) releases a replaced files buffer."""
         assert self._local is not None, "pinned slots need writer threads"
+        self.free = free
+        self._grow_lock = threading.Lock()
         for slot in range(self.n_slots):
             buf = alloc(self.slot_bytes)
             d = {k: np.ndarray(shape, np.dtype(dt), buffer=buf, offset=off)
@@ -168,8 +172,16 @@ class WriterPool:
         self.alloc = alloc
 
     def grow_files(self, slot: int, nbytes: int) -> np.ndarray:
-        """A larger ``files`` buffer for a slot (the batch's files did not fit)."""
-        self._local[slot]["files"] = self.alloc(nbytes)
+        """A larger ``files`` buffer for a slot (the batch's files did not
+        fit).  Called after :meth:`arrays` waited for the slot's tasks, so no
+        writer reads the old buffer: it is freed at once.  Render threads of
+        several renderers may grow at the same time; the allocator (one
+        renderer's context) is used under a lock."""
+        with self._grow_lock:
+            old = self._local[slot].get("files")
+            self._local[slot]["files"] = self.alloc(nbytes)
+            if old is not None and self.free is not None:
+                self.free(old)
         return self._local[slot]["files"]
 
     def arrays(self, slot: int) -> Dict[str, np.ndarray]:

@@ -16,7 +16,7 @@ import numpy as np
 
 from .build import IO_LIB, build_io, needs_build, IO_DEPS
 
-ABI_VERSION = 3  # CSGIO_ABI_VERSION in include/csg_io.h
+ABI_VERSION = 4  # CSGIO_ABI_VERSION in include/csg_io.h
 EXPORTED = ("csgio_abi_version", "csgio_write_png_rgb", "csgio_write_npy", "csgio_write_depth_csv",
             "csgio_write_pointcloud_txt", "csgio_depth_stats", "csgio_write_label_json")
 PNG_STRATEGY = {"default": 0, "rle": 1, "huffman": 2}
@@ -33,7 +33,8 @@ class Label(C.Structure):   # csgio_label
                 ("camera_pose", C.c_void_p), ("camera_params", C.c_char_p), ("class_mapping", C.c_char_p),
                 ("obj_head", C.c_void_p), ("obj_label", C.c_void_p), ("obj_kp_off", C.c_void_p),
                 ("obj_kp", C.c_void_p), ("inst_stats", C.c_void_p), ("covered", C.c_void_p),
-                ("kp_uv", C.c_void_p), ("kp_vis", C.c_void_p), ("kp_name", C.c_void_p)]
+                ("kp_uv", C.c_void_p), ("kp_vis", C.c_void_p), ("kp_name", C.c_void_p),
+                ("obj_listed", C.c_void_p)]
 
 
 def load() -> C.CDLL:
@@ -152,21 +153,31 @@ class LabelWriter:
         self._epochs[e] = st
         return st
 
-    def n_visible(self, ep: dict, inst_stats: np.ndarray) -> int:
+    def n_visible(self, ep: dict, inst_stats: np.ndarray, listed: Optional[np.ndarray] = None) -> int:
+        """Objects the label file lists: those with visible pixels (and, with
+        ``listed``, those flagged there; labels.label_record's rule)."""
         lab = ep["labels"][:ep["n"]]
         ok = (lab >= 0) & (lab < inst_stats.shape[0])
-        return int(np.count_nonzero(inst_stats[lab[ok], 0]))
+        vis = np.zeros(ep["n"], bool)
+        vis[ok] = inst_stats[lab[ok], 0] != 0
+        if listed is not None:
+            vis |= ok & np.asarray(listed, bool)[:ep["n"]]
+        return int(np.count_nonzero(vis))
 
     def write(self, path: str, frame_id: int, camera_pose, ep: dict, inst_stats: np.ndarray,
-              covered: Optional[np.ndarray], kp_uv: np.ndarray, kp_vis: np.ndarray) -> None:
+              covered: Optional[np.ndarray], kp_uv: np.ndarray, kp_vis: np.ndarray,
+              listed: Optional[np.ndarray] = None) -> None:
         pose = np.ascontiguousarray(np.asarray(camera_pose, np.float64).reshape(7))
         st = np.ascontiguousarray(inst_stats, np.uint32)
         cv = np.ascontiguousarray(covered, np.uint32) if covered is not None else None
         uv = np.ascontiguousarray(kp_uv, np.float32)
         vis = np.ascontiguousarray(kp_vis, np.int32)
+        lst = np.ascontiguousarray(listed, np.uint8) if listed is not None else None
+        if lst is not None and lst.shape[0] < ep["n"]:
+            raise CsgIoError(f"write_label_json: listed has {lst.shape[0]} entries, {ep['n']} objects")
         L = Label(int(frame_id), self.height, self.width, ep["n"], st.shape[0], self.n_kp, pose.ctypes.data,
                   self.camera_params, self.class_mapping, C.cast(ep["head_arr"], C.c_void_p).value,
                   ep["labels"].ctypes.data, ep["off"].ctypes.data, ep["idx"].ctypes.data, st.ctypes.data,
                   cv.ctypes.data if cv is not None else None, uv.ctypes.data, vis.ctypes.data,
-                  C.cast(self.kp_name, C.c_void_p).value)
+                  C.cast(self.kp_name, C.c_void_p).value, lst.ctypes.data if lst is not None else None)
         _check(load().csgio_write_label_json(path.encode(), C.byref(L)), "write_label_json", path)

@@ -29,7 +29,8 @@
  *   csg_outputs.file_kinds .... the frame's files encoded on the GPU:
  *                               cv2.imwrite of the RGB and JET depth
  *                               images, np.savetxt of the depth  :1672-1673,
- *                                                                :1687-1709
+ *                               and of the point cloud           :1687-1709,
+ *                                                                :714-775, :1716-1757
  *   csg_copy_files / csg_host_alloc / csg_host_free (pinned buffers for them)
  *   csg_last_error / csg_destroy
  *
@@ -161,6 +162,10 @@ typedef struct {
                                       byte-identical */
 #define CSG_FILE_DEPTH_PNG 4u      /* the JET depth visualisation (csg_outputs.depth_vis) as a PNG
                                       (GDP:1690-1709) */
+#define CSG_FILE_POINTCLOUD_TXT 8u /* np.savetxt(np.hstack([xyz, rgb]), fmt="%.6f", delimiter=" ",
+                                      header="x y z r g b", comments="") of the pixels with a point
+                                      (csg_outputs.points not NaN), row-major (GDP:766-770,
+                                      :1716-1757), byte-identical */
 
 typedef struct {
   uint64_t records;          /* raster triangles emitted (all frames of the last launch chain) */

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CSGIO_ABI_VERSION 3
+#define CSGIO_ABI_VERSION 4
 
 int csgio_abi_version(void);
 
@@ -64,7 +64,10 @@ int csgio_write_pointcloud_txt(const char* path, const float* xyz, const uint8_t
  * `obj_head[j]` as the fields of object j (inst_idx ... prim_path) indented
  * for level 3 ("      " before the first key), `kp_name[k]` as JSON string
  * literals.  Objects with no visible pixel (inst_stats[label][0] == 0, or a
- * label past n_labels) are left out, as label_record does. */
+ * label past n_labels) are left out, as label_record does, unless
+ * obj_listed[j] is 1 (the "frustum" object list: the object's 3D box meets the
+ * view frustum): then it is written with pixel_count 0, bbox_2d [-1, -1, -1,
+ * -1] and occlusion_ratio 1.0 (coverage known) or -1.0 (unknown). */
 typedef struct {
   uint32_t frame_id, height, width;
   uint32_t n_objects, n_labels, n_kp;
@@ -80,6 +83,7 @@ typedef struct {
   const float* kp_uv;                 /* [n_kp][2] */
   const int32_t* kp_vis;              /* [n_kp] */
   const char* const* kp_name;         /* [n_kp] */
+  const uint8_t* obj_listed;          /* [n_objects] 1: listed without visible pixels, or NULL */
 } csgio_label;
 
 int csgio_write_label_json(const char* path, const csgio_label* label);

@@ -7,6 +7,11 @@ independent decoders and writers:
   chunk CRC and the Adler-32 checked (tests/pngutil.py);
 * depth CSV (np.savetxt(depth, fmt="%.6f", delimiter=" "), :1687-1688):
   byte-identical to np.savetxt of the rendered depth;
+* point-cloud TXT (np.savetxt(np.hstack([xyz, rgb]), fmt="%.6f", delimiter=" ",
+  header="x y z r g b", comments=""), :766-770 and :1756-1757): byte-identical
+  to np.savetxt of the rendered points with a number and their RGB, in
+  row-major order (one 1080p frame; the others against the host writer,
+  itself byte-identical to np.savetxt in tests/test_writers.py);
 * the quality log's depth counts (csg_outputs.depth_stats, :318-341): equal
   to the host pass over the rendered depth (the float64 sum to 1e-12);
 
@@ -24,7 +29,7 @@ from pngutil import decode_png
 
 pytestmark = pytest.mark.gpu
 
-KINDS = ("rgb_png", "depth_csv", "depth_png")
+KINDS = ("rgb_png", "depth_csv", "depth_png", "pointcloud_txt")
 
 
 def _render(wl, frames, W=None, H=None, views=None, projs=None, cap=None):
@@ -37,8 +42,9 @@ def _render(wl, frames, W=None, H=None, views=None, projs=None, cap=None):
         for k, e in enumerate(epochs):
             r.set_instance_transforms(k, wl.epoch(e).models)
         fr = make_frames(views, projs, [epochs.index(f // 10) for f in frames], frames)
-        files = r.host_buffer(cap or len(frames) * H * W * 16 + (1 << 20))
-        out, offsets, need = r.render_files(fr, KINDS, files, want=("rgb", "depth", "depth_vis", "depth_stats"))
+        files = r.host_buffer(cap or len(frames) * H * W * 96 + (1 << 20))
+        out, offsets, need = r.render_files(fr, KINDS, files,
+                                            want=("rgb", "depth", "depth_vis", "depth_stats", "points"))
         if cap is not None:
             assert offsets is None and need > cap
             big = r.host_buffer(need)
@@ -49,27 +55,46 @@ def _render(wl, frames, W=None, H=None, views=None, projs=None, cap=None):
     return out, blobs
 
 
-def _check(out, blobs, n):
+def _pcd_savetxt(points, rgb):
+    ok = ~np.isnan(points).any(axis=-1)
+    ref = io.BytesIO()
+    np.savetxt(ref, np.hstack([points[ok], rgb[ok]]), fmt="%.6f", delimiter=" ", header="x y z r g b", comments="")
+    return ref.getvalue()
+
+
+def _pcd_host(points, rgb, tmp):
+    from constructionsceneposeestimation_amd import writers
+    writers.write_pointcloud_txt(str(tmp), points.reshape(-1, 3), rgb.reshape(-1, 3))
+    return open(tmp, "rb").read()
+
+
+def _check(out, blobs, n, tmp_path=None, savetxt_frames=(0,)):
     from constructionsceneposeestimation_amd.writers import depth_stats
+    nk = len(KINDS)
     for f in range(n):
         # the quality log's depth counts (csg_outputs.depth_stats) against the host pass
         ds, g = depth_stats(out["depth"][f]), out["depth_stats"][f]
         assert [int(g[0]), int(g[1]), int(g[2]), g[4], g[5]] == [ds["valid"], ds["zero"], ds["inf"], ds["min"], ds["max"]]
         assert abs(g[3] - ds["sum"]) <= 1e-12 * max(1.0, abs(ds["sum"]))
-        png, csv, dpng = blobs[3 * f:3 * f + 3]
+        png, csv, dpng, pcd = blobs[nk * f:nk * f + nk]
         assert np.array_equal(decode_png(png), out["rgb"][f]), f"frame {f}: rgb png"
         assert np.array_equal(decode_png(dpng), out["depth_vis"][f]), f"frame {f}: depth png"
         ref = io.BytesIO()
         np.savetxt(ref, out["depth"][f], fmt="%.6f", delimiter=" ")
         assert csv == ref.getvalue(), f"frame {f}: depth csv"
+        if f in savetxt_frames or tmp_path is None:
+            assert pcd == _pcd_savetxt(out["points"][f], out["rgb"][f]), f"frame {f}: point cloud txt"
+        else:
+            assert pcd == _pcd_host(out["points"][f], out["rgb"][f], tmp_path / f"pc{f}.txt"), f"frame {f}: pcd"
+        assert pcd.count(b"\n") == 1 + int((~np.isnan(out["points"][f]).any(axis=-1)).sum())
 
 
-def test_files_c3_1080p():
+def test_files_c3_1080p(tmp_path):
     from constructionsceneposeestimation_amd.workload import Workload
     wl = Workload("C3", seed=0)
     frames = [1200, 1517, 2323]
     out, blobs = _render(wl, frames)
-    _check(out, blobs, len(frames))
+    _check(out, blobs, len(frames), tmp_path)
     # compressed: the RGB PNG well below the raw image, the CSV at its text size
     assert len(blobs[0]) < 0.6 * 1920 * 1080 * 3
 
@@ -110,7 +135,7 @@ def test_generate_gpu_files_match_host_writers(tmp_path):
     generate(str(tmp_path / "gpu"), list(range(9)), writer_mode="thread", **kw)
     generate(str(tmp_path / "host"), list(range(9)), writer_mode="process", **kw)
     n = 0
-    for sub in ("rgb", "depth", "labels"):
+    for sub in ("rgb", "depth", "labels", "pointcloud"):
         names = sorted(os.listdir(tmp_path / "gpu" / sub))
         assert names == sorted(os.listdir(tmp_path / "host" / sub)) and names
         for name in names:
@@ -121,14 +146,14 @@ def test_generate_gpu_files_match_host_writers(tmp_path):
             else:
                 assert a == b, name
             n += 1
-    assert n == 9 * 5
+    assert n == 9 * 6
 
 
-def test_files_c5_4k():
+def test_files_c5_4k(tmp_path):
     """One C5 frame at 3840x2160 (22.5 PNG units and 60 CSV units per row,
     ~25 MB of raw RGB per image)."""
     from constructionsceneposeestimation_amd.workload import Workload
     wl = Workload("C5", seed=0)
     assert (wl.width, wl.height) == (3840, 2160)
     out, blobs = _render(wl, [1205])
-    _check(out, blobs, 1)
+    _check(out, blobs, 1, tmp_path, savetxt_frames=())

@@ -155,7 +155,7 @@ def test_domain_randomization_is_keyed_and_bounded(world2):
 
 def test_generate_cli_outputs_parse():
     from constructionsceneposeestimation_amd.generate import OUTPUTS, REFERENCE_OUTPUTS, parse_outputs
-    assert parse_outputs("reference") == REFERENCE_OUTPUTS == ("rgb", "mask", "depth_csv", "depth_png")
+    assert parse_outputs("reference") == REFERENCE_OUTPUTS == ("rgb", "mask", "depth_csv", "depth_png", "pointcloud")
     assert parse_outputs("all") == OUTPUTS
     assert parse_outputs("rgb, depth_npy") == ("rgb", "depth_npy")
     with pytest.raises(ValueError):

@@ -137,3 +137,79 @@ def test_native_label_writer_matches_python_label(tmp_path):
         lw.write(path, f, pose, ep, stats, cov, uv, vis)
         assert open(path, "rb").read() == labels.label_json_bytes(lab), f
         assert lw.n_visible(ep, stats) == lab["num_objects"]
+
+
+@pytest.mark.parametrize("mode", ["visible", "frustum"])
+def test_object_list_modes_native_and_python(tmp_path, mode):
+    """The label file's object list in both modes, on the same stats arrays
+    (DESIGN §10): "visible" lists objects with pixels; "frustum" also lists
+    the objects whose 3D box meets the view frustum (labels.in_frustum) with
+    pixel_count 0, bbox_2d [-1]*4 and occlusion_ratio 1.0 (-1.0 when the
+    coverage is unknown).  The native writer matches label_record byte for
+    byte in both."""
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd import labels
+    from constructionsceneposeestimation_amd.renderer import scene_labels
+    from constructionsceneposeestimation_amd.workload import Workload
+    from constructionsceneposeestimation_amd.writers import LabelWriter
+    wl = Workload("C3", seed=0)
+    nl, K = scene_labels(wl.scene), wl.n_keypoints()
+    lw = LabelWriter(wl.kp_table, wl.intr.params(), nl, wl.height, wl.width)
+    rng = np.random.default_rng(5)
+    n_hidden_listed = 0
+    for f in (3, 57, 118):
+        st = wl.epoch(f // 10)
+        poses = labels.object_poses(wl.scene, st.object_frames)
+        V, P, C = wl.camera(f)[:3]
+        inside = labels.in_frustum(wl.scene, st.object_frames, V, P, wl.width, wl.height, wl.intr.near, wl.intr.far)
+        assert 0 < inside.sum() < len(inside)   # a real camera sees some objects' boxes, not all
+        listed = inside if mode == "frustum" else None
+        stats = rng.integers(1, 1000, (nl, 5)).astype(np.uint32)
+        stats[rng.random(nl) < 0.5, 0] = 0
+        cov = rng.integers(0, 3000, nl).astype(np.uint32)
+        cov[rng.random(nl) < 0.2] |= 0x80000000
+        uv = (rng.standard_normal((K, 2)) * 800).astype(np.float32)
+        vis = rng.integers(0, 3, K).astype(np.int32)
+        pose = cm.get_obj_pose_from_matrix(C)
+        lab = labels.label_record(f, pose, wl.intr.params(), poses, stats, uv, vis, wl.kp_table, wl.height,
+                                  wl.width, covered=cov, listed=listed)
+        ids = [o["inst_idx"] for o in lab["objects"]]
+        by_idx = {p["inst_idx"]: j for j, p in enumerate(poses)}
+        want = [p["inst_idx"] for j, p in enumerate(poses)
+                if stats[p["inst_idx"], 0] > 0 or (mode == "frustum" and inside[j])]
+        assert ids == want
+        for o in lab["objects"]:
+            if o["pixel_count"] == 0:
+                assert mode == "frustum" and inside[by_idx[o["inst_idx"]]]
+                assert o["bbox_2d"] == [-1, -1, -1, -1]
+                known = not (int(cov[o["inst_idx"]]) & 0x80000000)
+                assert o["occlusion_ratio"] == (1.0 if known else -1.0)
+                n_hidden_listed += 1
+        ep = lw.epoch(f // 10, poses)
+        path = str(tmp_path / f"label_{f}.json")
+        lw.write(path, f, pose, ep, stats, cov, uv, vis, listed=listed)
+        assert open(path, "rb").read() == labels.label_json_bytes(lab), f
+        assert lw.n_visible(ep, stats, listed) == lab["num_objects"]
+    assert (n_hidden_listed > 0) == (mode == "frustum")
+
+
+def test_in_frustum_box_cases():
+    """labels.in_frustum on hand-placed boxes: in front, behind, far beyond
+    the far plane, off to the side, and straddling the image edge."""
+    from types import SimpleNamespace
+
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd import labels
+    W, H = 320, 180
+    intr = cm.Intrinsics(W, H)
+    cam, aim = np.array([0.0, 0.0, 1.5]), np.array([10.0, 0.0, 1.5])   # looking along +x
+    V, P, _ = cm.frame_matrices(cam, cm.look_at_world_quat(cam, aim), intr)
+    objs = [SimpleNamespace(local_bounds=(np.array([-0.5, -0.5, -0.5]), np.array([0.5, 0.5, 0.5])))] * 5
+    at = [(5, 0, 1.5), (-5, 0, 1.5), (400, 0, 1.5), (5, 30, 1.5), (5, 5.5, 1.5)]   # half-width 5.2 m at x = 5
+    frames = []
+    for x, y, z in at:
+        M = np.eye(4)
+        M[:3, 3] = (x, y, z)
+        frames.append(M)
+    got = labels.in_frustum(SimpleNamespace(objects=objs), frames, V, P, W, H, intr.near, intr.far)
+    assert got.tolist() == [True, False, False, False, True]

@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=30)
     ap.add_argument("--batches", type=int, default=8)
-    ap.add_argument("--kinds", default="rgb_png,depth_csv,depth_png")
+    ap.add_argument("--kinds", default="rgb_png,depth_csv,depth_png,pointcloud_txt")
     a = ap.parse_args()
     kinds = tuple(a.kinds.split(","))
     wl = Workload("C3", seed=0)
@@ -34,7 +34,8 @@ def main():
             epochs = sorted({f // 10 for f in fb})
             batches.append((fb, epochs, wl.frame_params(fb)))
         r.set_keypoints(0, wl.epoch(120).keypoints)   # (the keypoint count shapes the outputs)
-        files = r.host_buffer(F * 13 * wl.width * wl.height)
+        per_px = {"rgb_png": 3, "depth_csv": 12, "depth_png": 3, "pointcloud_txt": 72}   # upper estimates
+        files = r.host_buffer(F * sum(per_px[k] for k in kinds) * wl.width * wl.height)
         spec = r.output_spec(F, want)
         host = {}
         for k, (shape, dt) in spec.items():
