@@ -11,10 +11,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_generate_two_rank_shards_union_equals_one_rank(tmp_path):
+@pytest.mark.parametrize("workload,size", [("C3", (160, 96)), ("C4", (480, 272))])
+def test_generate_two_rank_shards_union_equals_one_rank(tmp_path, workload, size):
+    """C3 small, and C4 (per-epoch lights and texture swaps) at 480x272, with
+    the reference's file set (RGB PNG, depth CSV + PNG, point cloud, mask,
+    label) plus the depth .npy."""
     from constructionsceneposeestimation_amd.generate import main
-    common = ["--frames", "40", "--workload", "C3", "--seed", "4", "--batch", "7", "--width", "160",
-              "--height", "96", "--depth-csv"]
+    common = ["--frames", "40", "--workload", workload, "--seed", "4", "--batch", "7", "--width", str(size[0]),
+              "--height", str(size[1]), "--depth-csv"]
     main(["--out", str(tmp_path / "one"), "--rank", "0", "--world", "1"] + common)
     for rank in (0, 1):
         main(["--out", str(tmp_path / "two"), "--rank", str(rank), "--world", "2"] + common)
@@ -25,7 +29,8 @@ def test_generate_two_rank_shards_union_equals_one_rank(tmp_path):
         owner = (f // 10) % 2
         counts[owner] += 1
         for rel in (f"rgb/rgb_{f:06d}.png", f"labels/instance_mask_{f:06d}.npy", f"labels/label_{f:06d}.json",
-                    f"depth/depth_{f:06d}.npy", f"depth/depth_{f:06d}.csv"):
+                    f"depth/depth_{f:06d}.npy", f"depth/depth_{f:06d}.csv", f"depth/depth_{f:06d}.png",
+                    f"pointcloud/pointcloud_{f:06d}.txt"):
             a = (one / rel).read_bytes()
             assert a == (shards[owner] / rel).read_bytes(), (f, rel)
             assert not (shards[1 - owner] / rel).exists(), (f, rel)

@@ -176,15 +176,16 @@ def test_c5_4k_all_outputs():
     assert (ora["instance"] >= 0).mean() > 0.05
 
 
-def test_c4_domain_randomization_batch():
+@pytest.mark.parametrize("size", [(480, 272), (1920, 1080)])
+def test_c4_domain_randomization_batch(size):
     """C4: frames of three epochs in one batch, each epoch with its own layout,
     lighting (dome tint/intensity, sun) and texture swap, bit-exact vs the
-    oracle configured per frame."""
+    oracle configured per frame; at 480x272 and at the config's 1920x1080."""
     from constructionsceneposeestimation_amd.packing import pack_scene
     from constructionsceneposeestimation_amd.renderer import Renderer, make_frames
     from constructionsceneposeestimation_amd.workload import Workload
     from oracle.oracle import Oracle
-    wl = Workload("C4", seed=5, width=480, height=272)
+    wl = Workload("C4", seed=5, width=size[0], height=size[1])
     frames = [3, 14, 27, 33]
     epochs = sorted({f // 10 for f in frames})
     views, projs = wl.frame_params(frames)
