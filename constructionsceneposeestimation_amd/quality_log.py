@@ -122,7 +122,11 @@ class QualityLog:
                 lo, hi = float(depth_range[0]), float(depth_range[1])   # the GPU's min / max (depth PNG)
             else:
                 lo, hi = ds["min"], ds["max"]
-            mean = ds["sum"] / n_valid                                  # float64 sum (the reference: np.mean)
+            # float64 sum / count.  Deliberate divergence: the
+            # reference's np.mean(valid_depth) (GDP:328) sums its float32 array
+            # pairwise in float32 and returns a float32; the two agree to ~1e-6
+            # relative (tests/test_labels.py), not in the logged low digits.
+            mean = ds["sum"] / n_valid
         else:
             lo = hi = mean = 0.0
         rec["depth"] = {"status": "valid", "valid_pixels": n_valid, "total_pixels": total,

@@ -81,3 +81,17 @@ def test_native_float_repr_random_doubles():
                          rng.random(20000).astype(np.float32).astype(np.float64)])
     bad = [x for x in xs.tolist() if m.repr_float(x) != repr(x)]
     assert not bad, bad[:5]
+
+
+def test_quality_log_depth_mean_vs_reference_float32_mean():
+    """The quality log's depth_mean (float64 sum / count, from the GPU's
+    depth_stats) against the reference's np.mean of the float32 valid depths
+    (GDP:324-328): a documented divergence in the low digits only."""
+    from constructionsceneposeestimation_amd.writers import depth_stats
+    rng = np.random.default_rng(3)
+    d = rng.uniform(0.5, 250.0, (1080, 1920)).astype(np.float32)
+    d[rng.random(d.shape) < 0.3] = np.inf
+    ds = depth_stats(d)
+    ours = ds["sum"] / ds["valid"]
+    ref = float(np.mean(d[np.isfinite(d) & (d > 0)]))
+    assert abs(ours - ref) <= 1e-6 * ref
