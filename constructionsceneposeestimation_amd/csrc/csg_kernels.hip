@@ -207,21 +207,6 @@ __device__ __forceinline__ bool alpha_pass(const uint32_t* aquad, const uint32_t
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
 
-// 1/x rounded as IEEE division, for x in [2^-9, 2^9] (inverse depths; the
-// near/far range of the spec): the hardware reciprocal (< 1 ulp) and one
-// Newton step with fused residual.  CSG_FAST_RCP=0: the division itself.
-#ifndef CSG_FAST_RCP
-#define CSG_FAST_RCP 0
-#endif
-__device__ __forceinline__ float rcp_depth(float x) {
-#if CSG_FAST_RCP
-  const float r = __builtin_amdgcn_rcpf(x);
-  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
-#else
-  return 1.0f / x;
-#endif
-}
-
 // ---------------------------------------------------------------------------
 // wave / block helpers (wave64)
 // ---------------------------------------------------------------------------
@@ -333,16 +318,6 @@ __global__ __launch_bounds__(256) void k_clip(SceneDev s, BatchDev b) {
     }
     frame_camera(fr.view, fr.proj, b.cam + (size_t)f * kCamFloats);
   }
-}
-
-// 1/w of a clip-space vertex (w >= near): as rcp_depth below 2^64, the
-// division above (never taken by a real scene).
-__device__ __forceinline__ float rcp_w(float x) {
-  if (x < 0x1p64f) {
-    const float r = __builtin_amdgcn_rcpf(x);
-    return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
-  }
-  return 1.0f / x;
 }
 
 // ---------------------------------------------------------------------------
@@ -565,11 +540,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
       auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
         // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c)
         float su[3], sv[3];
-#if CSG_FAST_RCP >= 2
-        const float ra = rcp_w(a.w), rb = rcp_w(bb.w), rc = rcp_w(cc.w);
-#else
         const float ra = 1.0f / a.w, rb = 1.0f / bb.w, rc = 1.0f / cc.w;
-#endif
         su[0] = a.x * ra; sv[0] = a.y * ra;
         su[1] = bb.x * rb; sv[1] = bb.y * rb;
         su[2] = cc.x * rc; sv[2] = cc.y * rc;
@@ -1021,7 +992,7 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
   // alpha test at the pixel centre: u = U(x, y) * (1 / (1/W)), v likewise
   auto alpha_ok = [&]() {
     const uint4 g4 = I.q[4][k], g5 = I.q[5][k];
-    const float r = rcp_depth(invw);
+    const float r = 1.0f / invw;
     const float u = plane_at(f_(g3.y), f_(g3.z), f_(g3.w), fx, fy) * r;
     const float v = plane_at(f_(g4.x), f_(g4.y), f_(g4.z), fx, fy) * r;
     return alpha_pass(c.aquad, c.acls, g2.y, g4.w, (int)g5.x, u, v);
@@ -1378,7 +1349,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
   const bool textured = e.tex >= 0 && !(DBG(s.dbg) & 4096u);   // 4096: ablation only, no texture fetch
   const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
   float r = INFINITY;
-  if (need_depth || textured) r = rcp_depth(plane_at(e.P[0], e.P[1], e.P[2], fx, fy));
+  if (need_depth || textured) r = 1.0f / plane_at(e.P[0], e.P[1], e.P[2], fx, fy);
   depth_out = need_depth ? r : INFINITY;
   id_out = e.label;
   int base[3] = {(int)(e.base & 255u), (int)((e.base >> 8) & 255u), (int)((e.base >> 16) & 255u)};
@@ -1412,8 +1383,6 @@ static_assert(kShadeSlots <= (uint32_t)kBlock && kShadeSlots < 255u, "one setup 
 constexpr int kShadeProbes = 16;
 struct ResolveLds {
   uint32_t keys[kShadeSlots];       // uid or kNoAlpha (empty)
-  uint8_t dense[kShadeSlots];       // the round's occupied slots, in insertion order
-  uint32_t nused;                   // occupied slots of the round
   uint32_t more;                    // a pixel is left for another round
   ShadeEntry tab[kShadeSlots];
   uint32_t lstat[3][kMaxLdsLabels]; // per label: pixel count, column mask, row mask (tile-relative bits)
@@ -1446,18 +1415,13 @@ static_assert((sizeof(RasterSide<true>) > sizeof(ResolveLds) ? sizeof(RasterSide
               "k_raster<true> LDS must allow CSG_COV_WAVES workgroups per CU");
 
 // Slot of `uid` in the table (inserting it), or -1 if the probe run is full.
-// A slot taken here is also appended to the round's dense list, so that the
-// setup phase runs on threads 0..nused-1 (one or two waves) rather than on the
-// threads of the hashed slot indices (spread over 0..kShadeSlots-1: two waves
-// each issuing the whole setup).
-__device__ __forceinline__ int shade_slot(uint32_t* keys, uint8_t* dense, uint32_t* nused, uint32_t uid) {
+__device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
   const uint32_t h = __umulhi(uid * 2654435761u, kShadeSlots);   // [0, kShadeSlots)
 #pragma clang loop vectorize(disable) unroll(disable)
   for (int p = 0; p < kShadeProbes; ++p) {
     uint32_t idx = h + (uint32_t)p;
     idx = idx >= kShadeSlots ? idx - kShadeSlots : idx;
     const uint32_t prev = atomicCAS(&keys[idx], kNoAlpha, uid);
-    if (prev == kNoAlpha) dense[atomicAdd(nused, 1u)] = (uint8_t)idx;
     if (prev == kNoAlpha || prev == uid) return (int)idx;
   }
   return -1;
@@ -1678,7 +1642,6 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   // hoist per-pixel invariants across the setup phase, where they would spill.
   auto round = [&](const bool first) __attribute__((always_inline)) -> bool {
     if ((uint32_t)tid < kShadeSlots) L.q.keys[tid] = kNoAlpha;
-    if (tid == 0) L.q.nused = 0u;
     __syncthreads();
     // every thread has read the previous round's flag (it reached this
     // barrier) and none sets it before the next barrier
@@ -1705,7 +1668,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
           uint32_t sl;
           if (uid == prev_uid) sl = prev_slot;
           else {
-            const int r = shade_slot(L.q.keys, L.q.dense, &L.q.nused, uid);
+            const int r = shade_slot(L.q.keys, uid);
             sl = r < 0 ? 0xFFu : (uint32_t)r;
           }
           prev_uid = uid;
@@ -1718,10 +1681,9 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     }
     __syncthreads();
     {  // one thread per occupied slot: set the triangle up once for the whole tile
-      const uint32_t sl = (uint32_t)tid < L.q.nused ? L.q.dense[tid] : 0xFFu;
-      if (sl != 0xFFu) {
-        const uint32_t u = L.q.keys[sl];
-        ShadeEntry& e = L.q.tab[sl];
+      const uint32_t u = (uint32_t)tid < kShadeSlots ? L.q.keys[tid] : kNoAlpha;
+      if (u != kNoAlpha) {
+        ShadeEntry& e = L.q.tab[tid];
         if (DBG(b.dbg) & 8192u) {   // ablation only: no triangle setup (garbage shading)
           e = ShadeEntry{};
           e.P[2] = 1.0f; e.tex = -1; e.label = 0;
