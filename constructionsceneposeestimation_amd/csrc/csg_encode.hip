@@ -345,10 +345,13 @@ __global__ __launch_bounds__(256) void k_png_layout(EncPng* __restrict__ png, ui
 // short); lane i owns pixel i.  The length pass reduces the lanes' text
 // lengths to the unit's; the emit pass scans them, each lane formats its text
 // into the wave's LDS buffer at its offset, and the wave copies the buffer to
-// the file with coalesced dword stores (the unaligned ends as bytes).  A unit
-// whose text does not fit the buffer (values past ~1e30) writes lane by lane.
-constexpr uint32_t kTxtWaves = 4;          // units per 256-thread workgroup
-constexpr uint32_t kTxtBuf = 6144;         // LDS bytes per wave (64 typical point lines need ~4 KB)
+// the file with coalesced dword stores (the unaligned ends as bytes).  The
+// buffer holds 64 texts of the longest possible length, so every unit fits.
+constexpr uint32_t kTxtWaves = 4;          // length passes: units per 256-thread workgroup
+constexpr uint32_t kCsvWaves = 4;          // k_csv_emit: 4 x 3 KB of LDS per workgroup
+constexpr uint32_t kPcdWaves = 2;          // k_pcd_emit: 2 x 11.3 KB
+constexpr uint32_t kCsvBuf = 64u * (kMaxF6Chars + 1);   // LDS bytes per wave: a value and its separator
+constexpr uint32_t kPcdBuf = 64u * kMaxPcdLine + kPcdHeaderBytes;
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -654,21 +657,13 @@ __global__ __launch_bounds__(64) void k_png_pack(const EncPng* __restrict__ png,
   o.finish();
 }
 
-// A lane's text written straight to the file when the unit overflows the LDS buffer.
-__device__ __noinline__ void put_text_direct(uint8_t* out, uint64_t pos, const char* s, int n) {
-  ByteOut o;
-  o.init(out, pos);
-  for (int k = 0; k < n; ++k) o.put((uint8_t)s[k]);
-  o.finish();
-}
-
-__global__ __launch_bounds__(64 * kTxtWaves) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
+__global__ __launch_bounds__(64 * kCsvWaves) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
                                                              const uint32_t* __restrict__ uoff, uint8_t* out,
                                                              const uint64_t* __restrict__ foff, uint32_t nk,
                                                              uint32_t kslot) {
-  __shared__ uint32_t tbuf[kTxtWaves][kTxtBuf / 4 + 1];
+  __shared__ uint32_t tbuf[kCsvWaves][kCsvBuf / 4 + 1];
   const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t u = blockIdx.x * kTxtWaves + wv;
+  const uint32_t u = blockIdx.x * kCsvWaves + wv;
   if (u >= H * V) return;
   uint32_t r, x0, x1;
   txt_unit(u, V, W, r, x0, x1);
@@ -679,15 +674,6 @@ __global__ __launch_bounds__(64 * kTxtWaves) void k_csv_emit(const float* __rest
   const uint32_t off = wave_excl_scan(n, lane, total);
   const uint64_t pos = foff[(size_t)f * nk + kslot] + uoff[(size_t)f * H * V + u];
   const char sep = x + 1u < W ? ' ' : '\n';
-  if (total > kTxtBuf) {
-    if (n) {
-      char tmp[kMaxF6Chars + 1];
-      const int k = fmt6f(d, tmp);
-      tmp[k] = sep;
-      put_text_direct(out, pos + off, tmp, k + 1);
-    }
-    return;
-  }
   char* t = reinterpret_cast<char*>(tbuf[wv]);
   if (n) {
     fmt6f(d, t + off);
@@ -699,13 +685,13 @@ __global__ __launch_bounds__(64 * kTxtWaves) void k_csv_emit(const float* __rest
   wave_copy_out(tbuf[wv], total, out, pos, lane);
 }
 
-__global__ __launch_bounds__(64 * kTxtWaves) void k_pcd_emit(const float* __restrict__ pts, const uint8_t* __restrict__ rgb,
+__global__ __launch_bounds__(64 * kPcdWaves) void k_pcd_emit(const float* __restrict__ pts, const uint8_t* __restrict__ rgb,
                                                              uint32_t W, uint32_t H, const uint32_t* __restrict__ uoff,
                                                              uint8_t* out, const uint64_t* __restrict__ foff,
                                                              uint32_t nk, uint32_t kslot) {
-  __shared__ uint32_t tbuf[kTxtWaves][kTxtBuf / 4 + 1];
+  __shared__ uint32_t tbuf[kPcdWaves][kPcdBuf / 4 + 1];
   const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t u = blockIdx.x * kTxtWaves + wv;
+  const uint32_t u = blockIdx.x * kPcdWaves + wv;
   if (u >= H * V) return;
   uint32_t r, x0, x1;
   txt_unit(u, V, W, r, x0, x1);
@@ -727,15 +713,6 @@ __global__ __launch_bounds__(64 * kTxtWaves) void k_pcd_emit(const float* __rest
   const uint32_t off = wave_excl_scan(n, lane, total) + hdr;
   total += hdr;
   const uint64_t pos = foff[(size_t)f * nk + kslot] + uoff[(size_t)f * H * V + u];
-  if (total > kTxtBuf) {
-    if (lane < hdr) out[pos + lane] = (uint8_t)pcd_header_byte(lane);
-    if (n) {
-      char tmp[kMaxPcdLine];
-      const int k = pcd_line(X, Y, Z, R, G, B, tmp);
-      put_text_direct(out, pos + off, tmp, k);
-    }
-    return;
-  }
   char* t = reinterpret_cast<char*>(tbuf[wv]);
   if (lane < hdr) t[lane] = pcd_header_byte(lane);
   if (n) pcd_line(X, Y, Z, R, G, B, t + off);
@@ -878,14 +855,14 @@ void launch_depth_stats(const float* depth, uint32_t npx, uint32_t F, void* scra
 void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,
                      const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
   const uint32_t n = csv_units_per_frame(W, H);
-  hipLaunchKernelGGL(k_csv_emit, dim3((n + kTxtWaves - 1) / kTxtWaves, F), dim3(64 * kTxtWaves), 0, st, depth, W, H,
+  hipLaunchKernelGGL(k_csv_emit, dim3((n + kCsvWaves - 1) / kCsvWaves, F), dim3(64 * kCsvWaves), 0, st, depth, W, H,
                      rowoff, out, foff, nk, kslot);
 }
 
 void launch_pcd_emit(const float* points, const uint8_t* rgb, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff,
                      uint8_t* out, const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
   const uint32_t n = csv_units_per_frame(W, H);
-  hipLaunchKernelGGL(k_pcd_emit, dim3((n + kTxtWaves - 1) / kTxtWaves, F), dim3(64 * kTxtWaves), 0, st, points, rgb,
+  hipLaunchKernelGGL(k_pcd_emit, dim3((n + kPcdWaves - 1) / kPcdWaves, F), dim3(64 * kPcdWaves), 0, st, points, rgb,
                      W, H, rowoff, out, foff, nk, kslot);
 }
 
