@@ -346,12 +346,11 @@ __global__ __launch_bounds__(256) void k_png_layout(EncPng* __restrict__ png, ui
 // lengths to the unit's; the emit pass scans them, each lane formats its text
 // into the wave's LDS buffer at its offset, and the wave copies the buffer to
 // the file with coalesced dword stores (the unaligned ends as bytes).  The
-// buffer holds 64 texts of the longest possible length, so every unit fits.
-constexpr uint32_t kTxtWaves = 4;          // length passes: units per 256-thread workgroup
-constexpr uint32_t kCsvWaves = 4;          // k_csv_emit: 4 x 3 KB of LDS per workgroup
-constexpr uint32_t kPcdWaves = 2;          // k_pcd_emit: 2 x 11.3 KB
-constexpr uint32_t kCsvBuf = 64u * (kMaxF6Chars + 1);   // LDS bytes per wave: a value and its separator
-constexpr uint32_t kPcdBuf = 64u * kMaxPcdLine + kPcdHeaderBytes;
+// buffer holds the texts of the longest possible length: 64 CSV values, or
+// the point lines of half a wave (k_pcd_emit runs the two halves in turn).
+constexpr uint32_t kTxtWaves = 4;          // units per 256-thread workgroup
+constexpr uint32_t kCsvBuf = 64u * (kMaxF6Chars + 1);              // 3.1 KB per wave: a value and its separator
+constexpr uint32_t kPcdBuf = 32u * kMaxPcdLine + kPcdHeaderBytes;   // 5.8 KB per wave
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -657,13 +656,13 @@ __global__ __launch_bounds__(64) void k_png_pack(const EncPng* __restrict__ png,
   o.finish();
 }
 
-__global__ __launch_bounds__(64 * kCsvWaves) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
+__global__ __launch_bounds__(64 * kTxtWaves) void k_csv_emit(const float* __restrict__ depth, uint32_t W, uint32_t H,
                                                              const uint32_t* __restrict__ uoff, uint8_t* out,
                                                              const uint64_t* __restrict__ foff, uint32_t nk,
                                                              uint32_t kslot) {
-  __shared__ uint32_t tbuf[kCsvWaves][kCsvBuf / 4 + 1];
+  __shared__ uint32_t tbuf[kTxtWaves][kCsvBuf / 4 + 1];
   const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t u = blockIdx.x * kCsvWaves + wv;
+  const uint32_t u = blockIdx.x * kTxtWaves + wv;
   if (u >= H * V) return;
   uint32_t r, x0, x1;
   txt_unit(u, V, W, r, x0, x1);
@@ -685,13 +684,13 @@ __global__ __launch_bounds__(64 * kCsvWaves) void k_csv_emit(const float* __rest
   wave_copy_out(tbuf[wv], total, out, pos, lane);
 }
 
-__global__ __launch_bounds__(64 * kPcdWaves) void k_pcd_emit(const float* __restrict__ pts, const uint8_t* __restrict__ rgb,
+__global__ __launch_bounds__(64 * kTxtWaves) void k_pcd_emit(const float* __restrict__ pts, const uint8_t* __restrict__ rgb,
                                                              uint32_t W, uint32_t H, const uint32_t* __restrict__ uoff,
                                                              uint8_t* out, const uint64_t* __restrict__ foff,
                                                              uint32_t nk, uint32_t kslot) {
-  __shared__ uint32_t tbuf[kPcdWaves][kPcdBuf / 4 + 1];
+  __shared__ uint32_t tbuf[kTxtWaves][kPcdBuf / 4 + 1];
   const uint32_t f = blockIdx.y, V = csv_units(W), lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t u = blockIdx.x * kPcdWaves + wv;
+  const uint32_t u = blockIdx.x * kTxtWaves + wv;
   if (u >= H * V) return;
   uint32_t r, x0, x1;
   txt_unit(u, V, W, r, x0, x1);
@@ -713,13 +712,25 @@ __global__ __launch_bounds__(64 * kPcdWaves) void k_pcd_emit(const float* __rest
   const uint32_t off = wave_excl_scan(n, lane, total) + hdr;
   total += hdr;
   const uint64_t pos = foff[(size_t)f * nk + kslot] + uoff[(size_t)f * H * V + u];
+  // lanes 0-31 (and the header), then lanes 32-63: each half's text is a
+  // contiguous range of the unit's
+  const uint32_t split = __shfl(off, 32, 64);
   char* t = reinterpret_cast<char*>(tbuf[wv]);
-  if (lane < hdr) t[lane] = pcd_header_byte(lane);
-  if (n) pcd_line(X, Y, Z, R, G, B, t + off);
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  wave_copy_out(tbuf[wv], total, out, pos, lane);
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint32_t lo = h ? split : 0u, hi = h ? total : split;
+    if ((lane >> 5) == h) {
+      if (lane < hdr) t[lane] = pcd_header_byte(lane);
+      if (n) pcd_line(X, Y, Z, R, G, B, t + (off - lo));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_copy_out(tbuf[wv], hi - lo, out, pos + lo, lane);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -855,14 +866,14 @@ void launch_depth_stats(const float* depth, uint32_t npx, uint32_t F, void* scra
 void launch_csv_emit(const float* depth, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff, uint8_t* out,
                      const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
   const uint32_t n = csv_units_per_frame(W, H);
-  hipLaunchKernelGGL(k_csv_emit, dim3((n + kCsvWaves - 1) / kCsvWaves, F), dim3(64 * kCsvWaves), 0, st, depth, W, H,
+  hipLaunchKernelGGL(k_csv_emit, dim3((n + kTxtWaves - 1) / kTxtWaves, F), dim3(64 * kTxtWaves), 0, st, depth, W, H,
                      rowoff, out, foff, nk, kslot);
 }
 
 void launch_pcd_emit(const float* points, const uint8_t* rgb, uint32_t W, uint32_t H, uint32_t F, const uint32_t* rowoff,
                      uint8_t* out, const uint64_t* foff, uint32_t nk, uint32_t kslot, hipStream_t st) {
   const uint32_t n = csv_units_per_frame(W, H);
-  hipLaunchKernelGGL(k_pcd_emit, dim3((n + kPcdWaves - 1) / kPcdWaves, F), dim3(64 * kPcdWaves), 0, st, points, rgb,
+  hipLaunchKernelGGL(k_pcd_emit, dim3((n + kTxtWaves - 1) / kTxtWaves, F), dim3(64 * kTxtWaves), 0, st, points, rgb,
                      W, H, rowoff, out, foff, nk, kslot);
 }
 

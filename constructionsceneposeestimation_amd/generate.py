@@ -300,13 +300,16 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 _log_done(log, *pending.pop(0), "pointcloud" in outs)
         for p in pending:
             _log_done(log, *p, "pointcloud" in outs)
+        t_done = time.time()   # every file written (teardown below: freeing page-locked buffers)
     finally:
         ahead.shutdown(wait=True)
         prep.shutdown(wait=True)
         pool.close()
+        t_close = time.time()
         for x in rends:
             x.close()
-    wall = time.time() - t0
+    wall = t_done - t0
+    t_teardown = time.time() - t_close
     log.save()
     summary = log.summary()
     summary["throughput"] = {"frames": len(frames), "wall_s": round(wall, 3), "render_s": round(t_render, 3),
@@ -315,6 +318,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                              "main_thread": {"wait_render_s": round(t_main_wait, 3), "labels_s": round(t_labels, 3)},
                              "frames_per_s": round(len(frames) / wall, 2) if wall > 0 else None,
                              "writers": n_writers, "writer_mode": writer_mode, "renderers": n_rend,
+                             "writer_task_s": round(pool.task_s, 3), "teardown_s": round(t_teardown, 3),
+                             "writer_busy": round(pool.task_s / (wall * n_writers), 3) if wall > 0 else None,
                              "outputs": sorted(outs)}
     return summary
 

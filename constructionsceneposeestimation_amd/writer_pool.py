@@ -25,6 +25,7 @@ from __future__ import annotations
 import multiprocessing as mp
 import os
 import threading
+import time
 from concurrent.futures import Future, ProcessPoolExecutor, ThreadPoolExecutor
 from typing import Dict, List, Optional, Tuple
 
@@ -128,6 +129,8 @@ class WriterPool:
 
     def __init__(self, spec: Dict[str, tuple], workers: int, n_slots: int = 3, mode: str = "process"):
         self.mode = mode
+        self.workers = workers
+        self.task_s, self.tasks = 0.0, 0   # thread mode: summed wall time of the frame tasks
         self.layout: Layout = {}
         off = 0
         for k, (shape, dt) in spec.items():
@@ -148,6 +151,7 @@ class WriterPool:
             self._local = None
         elif mode == "thread":
             self.pool = ThreadPoolExecutor(max_workers=workers)
+            self._task_lock = threading.Lock()
             self._local = [{k: np.empty(shape, np.dtype(dt)) for k, (_, shape, dt) in self.layout.items()}
                            for _ in range(n_slots)]
         else:
@@ -200,9 +204,20 @@ class WriterPool:
             f = self.pool.submit(_task, self.shm.name, self.slot_bytes, self.layout, slot, k, files, label,
                                  label_path)
         else:
-            f = self.pool.submit(write_frame, self._local[slot], k, files, label, label_path)
+            f = self.pool.submit(self._timed_write, self._local[slot], k, files, label, label_path)
         self.busy[slot].append(f)
         return f
+
+    def _timed_write(self, *args):
+        """write_frame in a writer thread, its wall time added to ``task_s``."""
+        t0 = time.perf_counter()
+        try:
+            return write_frame(*args)
+        finally:
+            dt = time.perf_counter() - t0
+            with self._task_lock:
+                self.task_s += dt
+                self.tasks += 1
 
     def close(self) -> None:
         for fs in self.busy:
