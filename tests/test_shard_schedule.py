@@ -98,13 +98,14 @@ def _worker(rank, world, port, total, out_dir):
 
 
 @pytest.mark.slow
-def test_two_rank_gloo_union_equals_single_process(tmp_path):
-    """world_size-2 run over gloo: each rank renders only its epochs; the union
-    is bit-identical to a single-process render of every frame."""
+@pytest.mark.parametrize("world,total", [(2, 40), (4, 80)])
+def test_multi_rank_gloo_union_equals_single_process(tmp_path, world, total):
+    """world_size-2 and -4 runs over gloo: each rank renders only its epochs;
+    the union is bit-identical to a single-process render of every frame
+    (shards at n = 2/4 union to n = 1)."""
     import pickle
     import torch.multiprocessing as mp
-    total = 40
-    mp.spawn(_worker, args=(2, _free_port(), total, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), total, str(tmp_path)), nprocs=world, join=True)
     gathered = pickle.load(open(tmp_path / "gathered.pkl", "rb"))
     union = {}
     for part in gathered:
@@ -116,7 +117,7 @@ def test_two_rank_gloo_union_equals_single_process(tmp_path):
     from oracle.oracle import Oracle
     wl = Workload("C3", seed=5, width=64, height=36)
     o = Oracle(pack_scene(wl.scene), wl.width, wl.height)
-    for f in (0, 13, 27, 39):
+    for f in (0, 13, 27, total - 1):
         o.set_instance_models(wl.epoch(f // 10).models.reshape(-1, 16))
         v, p = wl.frame_params([f])
         r = o.render(v[0], p[0])
