@@ -15,5 +15,8 @@ if [ $rc -eq 0 ]; then
     timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_files/$name -o pmc -- python3 tools/files_bench.py --batch 30 --batches 3 > gpurun_out/pmc_files/$name.json 2> gpurun_out/pmc_files/$name.err || { rc=$?; break; }
   done
 fi
+if [ $rc -eq 0 ]; then
+  ROUND=r03 PASSES="fetch write" bash tools/pmc_profile.sh > gpurun_out/pmc_r03_traffic.txt 2>&1 || rc=$?
+fi
 for w in C2 C4 C5; do python3 -c "import json; d=json.load(open('gpurun_out/cfg/bench_$w.json')); print('$w', d['value'], d['cpu_baseline'])" 2>/dev/null; done
 exit $rc

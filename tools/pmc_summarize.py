@@ -21,7 +21,8 @@ def load(d):
     for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
             name = row.get("Kernel_Name", "")
-            short = name.split("(")[0].replace("csg::", "").replace("void ", "").split("<")[0].strip()
+            short = (name.replace("(anonymous namespace)::", "").split("(")[0].replace("csg::", "")
+                     .replace("void ", "").split("<")[0].strip())
             per[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return per
 
