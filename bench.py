@@ -47,7 +47,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "annotated frames/sec (RGB+seg+2D kpts) at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-RECORD_BYTES = 96 + 4  # k_setup writes one 96-B raster record + its 4-B tile rectangle per record
+RECORD_BYTES = 80 + 4  # k_setup writes one 80-B raster record + its 4-B tile rectangle per record
 DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 240
 
 

@@ -599,8 +599,11 @@ static int sync_scene_state(csg_ctx* c) {
   size_t total = 0;
   for (size_t k = 0; k < c->textures.size(); ++k) {
     td[k] = TexDesc{(uint32_t)total, c->textures[k].w, c->textures[k].h, 0};
-    total += (size_t)c->textures[k].w * c->textures[k].h;
+    total += ((size_t)c->textures[k].w * c->textures[k].h + kTexAlign - 1) / kTexAlign * kTexAlign;
   }
+  // raster records carry a texture's offset / kTexAlign in 24 bits (Rec::atex)
+  if (total / kTexAlign >= 0xFFFFFFu)
+    return c->fail(CSG_ERR_LIMIT, "textures hold %zu texels; at most %u", total, 0xFFFFFFu * kTexAlign);
   if (c->tex_dirty) {
     HIP_TRY(c, c->texels.alloc(std::max<size_t>(total * 4, 4)));
     HIP_TRY(c, c->aquad.alloc(std::max<size_t>(total, 1)));

@@ -54,20 +54,21 @@ static_assert(sizeof(Chunk) == 48, "Chunk layout");
 // screen-space planes of its ORIGINAL triangle (spec §3.5-6): 1/W and, for
 // alpha-tested materials, u/W and v/W.  Field groups of 16 B as k_setup
 // writes and k_raster stages them: 0 x0 x1 x2 y0 | 1 y1 y2 p0 p1 |
-// 2 uid atex D0 D1 | 3 D2 U0 U1 U2 | 4 V0 V1 V2 atex_wh | 5 athr.
+// 2 uid atex D0 D1 | 3 D2 U0 U1 U2 | 4 V0 V1 V2 atex_wh.
 struct __attribute__((aligned(16))) Rec {
   int32_t x[3], y[3];          // 24: 24.8 fixed point, positive orientation
   uint16_t px0, py0, px1, py1; // 8 : inclusive pixel bbox, clamped to the frame
   uint32_t uid;                // 4
-  uint32_t atex;               // 4 : alpha-test texture, texel offset (kNoAlpha: none)
+  uint32_t atex;               // 4 : alpha test (kNoAlpha: none): texel offset / 16 | threshold << 24
+                               //     (keep iff alpha > threshold; texture offsets are 16-texel aligned)
   float D[3];                  // 12: 1/W = (D0*x + D1*y) + D2 at pixel centre (x, y)
   float U[3], V[3];            // 24: u/W, v/W planes (alpha-tested materials; zeros otherwise)
   uint32_t atex_wh;            // 4 : alpha texture width | height << 16
-  uint32_t athr;               // 4 : alpha threshold (keep iff alpha > athr)
-  uint32_t pad[3];             // 12
 };
-static_assert(sizeof(Rec) == 96, "Rec layout");
-constexpr int kRecGroups = 6;  // 16-B field groups (the 96 B of the record)
+static_assert(sizeof(Rec) == 80, "Rec layout");
+constexpr int kRecGroups = 5;  // 16-B field groups (the 80 B of the record)
+constexpr uint32_t kTexAlign = 16;   // texture offsets (texels) are multiples of this: Rec::atex packing
+__host__ __device__ inline uint32_t rec_atex(uint32_t offset, uint32_t thr) { return (offset / kTexAlign) | (thr << 24); }
 
 struct FrameDev {                // csg_frame mirror
   float view[16];

@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   // indexed, which would put them in scratch), groups 2-5 shared (the
   // original triangle's uid, alpha texture and planes).
   SubRec r0, r1;
-  uint4 c2 = make_uint4(0u, 0u, 0u, 0u), c3 = c2, c4 = c2, c5 = c2;
+  uint4 c2 = make_uint4(0u, 0u, 0u, 0u), c3 = c2, c4 = c2;
   int nrec = 0;
   if ((uint32_t)tid < ch.count) {
     const uint32_t g = ch.soup + tid;   // soup index (no instance-table load on the way)
@@ -563,7 +563,9 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
           nrec = 0;
         } else {
           const InstSetDev is = b.iset[(size_t)b.fset[f] * s.n_inst + i];
-          const uint32_t atex = is.atex, atex_wh = is.atex_wh, athr = is.athr;
+          // a threshold of 255 passes no fragment: such a record is not emitted
+          const uint32_t atex = is.atex == kNoAlpha ? kNoAlpha : rec_atex(is.atex, is.athr), atex_wh = is.atex_wh;
+          if (is.atex != kNoAlpha && is.athr >= 255u) nrec = 0;
           float D[3], U[3] = {0.0f, 0.0f, 0.0f}, V[3] = {0.0f, 0.0f, 0.0f};
           depth_plane(h.A, h.B, h.C, h.invdet, D);
           if (is.alpha_uv) {   // uvs loaded only now: few values live at once
@@ -576,7 +578,6 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
           c2 = make_uint4(uid, atex, __float_as_uint(D[0]), __float_as_uint(D[1]));
           c3 = make_uint4(__float_as_uint(D[2]), __float_as_uint(U[0]), __float_as_uint(U[1]), __float_as_uint(U[2]));
           c4 = make_uint4(__float_as_uint(V[0]), __float_as_uint(V[1]), __float_as_uint(V[2]), atex_wh);
-          c5 = make_uint4(athr, 0u, 0u, 0u);
         }
       }
     }
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   if (lane == 0 && wtot) wbase = atomicAdd(&b.rec_count[f * kCounterStride], wtot);
   wbase = __shfl(wbase, 0, 64);
   if (DBG(b.dbg) & 128u) {   // ablation: no record stores
-    if (nrec == 3 && b.inst) b.inst[0] = r0.g0.x + r1.g0.x + c2.x + c3.x + c4.x + c5.x;
+    if (nrec == 3 && b.inst) b.inst[0] = r0.g0.x + r1.g0.x + c2.x + c3.x + c4.x;
     return;
   }
   // Coalesced record stores.  The wave's records take the contiguous slots
@@ -612,7 +613,6 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     o[2] = c2;
     o[3] = c3;
     o[4] = c4;
-    o[5] = c5;
   };
   for (uint32_t p0 = 0; p0 < wtot; p0 += 16) {
     if (nrec > 0 && mine - p0 < 16u) put(mine - p0, r0);
@@ -893,7 +893,7 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // 256-thread workgroups per CU need <= 22 KiB of LDS each (104 staged records,
 // 116 shade-table slots) and <= 72 VGPRs.
 #ifndef CSG_STAGE
-#define CSG_STAGE 104
+#define CSG_STAGE 120
 #endif
 #ifndef CSG_WAVES
 #define CSG_WAVES 7             // k_raster waves per SIMD to budget registers for
@@ -991,11 +991,11 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
   // alpha test at the pixel centre: u = U(x, y) * (1 / (1/W)), v likewise
   auto alpha_ok = [&]() {
-    const uint4 g4 = I.q[4][k], g5 = I.q[5][k];
+    const uint4 g4 = I.q[4][k];
     const float r = 1.0f / invw;
     const float u = plane_at(f_(g3.y), f_(g3.z), f_(g3.w), fx, fy) * r;
     const float v = plane_at(f_(g4.x), f_(g4.y), f_(g4.z), fx, fy) * r;
-    return alpha_pass(c.aquad, c.acls, g2.y, g4.w, (int)g5.x, u, v);
+    return alpha_pass(c.aquad, c.acls, (g2.y & 0xFFFFFFu) * kTexAlign, g4.w, (int)(g2.y >> 24), u, v);
   };
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
