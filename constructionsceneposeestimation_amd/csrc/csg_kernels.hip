@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   }
 
   // Records: groups 0-1 per sub-triangle (r0, r1: named, never runtime-
-  // indexed, which would put them in scratch), groups 2-5 shared (the
+  // indexed, which would put them in scratch), groups 2-4 shared (the
   // original triangle's uid, alpha texture and planes).
   SubRec r0, r1;
   uint4 c2 = make_uint4(0u, 0u, 0u, 0u), c3 = c2, c4 = c2;
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     return;
   }
   // Coalesced record stores.  The wave's records take the contiguous slots
-  // [wbase, wbase + wtot), but lane-by-lane 16-B stores at a 96-B stride
+  // [wbase, wbase + wtot), but lane-by-lane 16-B stores at an 80-B stride
   // write many more partial 128-B lines than the bytes need.  So, 16 records
   // at a time, the lanes holding them put them in a per-wave LDS stage and the
   // wave stores the stage as consecutive 16-B chunks (1 KB per instruction).
@@ -881,7 +881,7 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // ---------------------------------------------------------------------------
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
-// LDS image of up to kStage staged records as their six 16-B field groups (see
+// LDS image of up to kStage staged records as their five 16-B field groups (see
 // Rec), group-major: lanes reading one group of different records hit
 // consecutive 16-B slots (no bank conflicts; a record-strided image puts 8
 // records on each set of banks), lanes reading the same record broadcast.
@@ -890,8 +890,8 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // waves per SIMD are its lever (measured on C3 against 4 waves: 3 waves +22%
 // time, 5 waves -8%, 6 waves a further -5%; with 96-B records 7 waves a
 // further -4%, 8 waves lose again to spills and small batches).  Seven
-// 256-thread workgroups per CU need <= 22 KiB of LDS each (104 staged records,
-// 116 shade-table slots) and <= 72 VGPRs.
+// 256-thread workgroups per CU need <= 22 KiB of LDS each (120 staged 80-B
+// records, 116 shade-table slots) and <= 72 VGPRs.
 #ifndef CSG_STAGE
 #define CSG_STAGE 120
 #endif
