@@ -890,16 +890,16 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // waves per SIMD are its lever (measured on C3 against 4 waves: 3 waves +22%
 // time, 5 waves -8%, 6 waves a further -5%; with 96-B records 7 waves a
 // further -4%, 8 waves lose again to spills and small batches).  Seven
-// 256-thread workgroups per CU need <= 22 KiB of LDS each (120 staged 80-B
+// 256-thread workgroups per CU need <= 22 KiB of LDS each (124 staged 80-B
 // records, 116 shade-table slots) and <= 72 VGPRs.
 #ifndef CSG_STAGE
-#define CSG_STAGE 120
+#define CSG_STAGE 124
 #endif
 #ifndef CSG_WAVES
 #define CSG_WAVES 7             // k_raster waves per SIMD to budget registers for
 #endif
 #ifndef CSG_COV_STAGE
-#define CSG_COV_STAGE 64        // k_raster<true>: smaller batches pay for the coverage table (7 workgroups per CU)
+#define CSG_COV_STAGE 72        // k_raster<true>: smaller batches pay for the coverage table (7 workgroups per CU)
 #endif
 #ifndef CSG_COV_WAVES
 #define CSG_COV_WAVES 7
@@ -1110,7 +1110,7 @@ struct RasterLds {
   uint32_t starts1[NS];                 // bit i: a staged record's rows start at level-1 item i
   uint16_t before1[NS + 1];             // records starting before item 32*d
   uint32_t crec[NS];                    // compact record: slot | first item << 8
-  uint8_t row0[kBlock];                 // first tile row of each staged record | 0x80 if small
+  uint8_t row0[NS];                     // first tile row of each staged record | 0x80 if small
   uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
   uint32_t starts[kBlock];              // bit i: a span starts at level-2 item i (<= 256 spans x 32 px)
   uint16_t before[kBlock + 1];          // spans starting before item 32*d
@@ -1130,7 +1130,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
   for (uint32_t base = beg; base < end; base += NS) {
     uint32_t row0;
     const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
-    L.row0[tid] = (uint8_t)row0;
+    if (tid < NS) L.row0[tid] = (uint8_t)row0;
     if constexpr (kCov) {   // label of the staged record (read back from this thread's own slot)
       if (tid < NS) {
         int32_t lab = -1;
