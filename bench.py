@@ -147,7 +147,7 @@ def roofline(b_geom: int, b_tex: int, b_out: int, frames_per_launch: float, rast
              "B_geom, which k_setup reads)"),
         kern("k_setup", round(b_geom + frames_per_launch * records_per_frame * RECORD_BYTES), setup_ms,
              "B_geom once per launch (the launch's frames share the geometry through L2 and the Infinity "
-             "Cache: the grid runs frame-fast) + 100 B written per raster record (k_clip + k_setup)"),
+             "Cache: the grid runs frame-fast) + 84 B written per raster record: the 80-B record and its 4-B tile rectangle"),
     ]
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic.get("k_raster"),
@@ -244,6 +244,9 @@ def main():
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--frames-per-launch", type=int, default=0, help="frames per kernel chain (0 = library default)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--contexts", type=int, default=1,
+                    help="renderer contexts per GPU, each with its own stream, work buffers and output buffers; "
+                         "steps alternate between them so one step's short kernels overlap the other's k_raster")
     ap.add_argument("--verify-frames", type=int, default=32,
                     help="frames of the last timed step re-rendered by the oracle and compared (rank 0 at N=1: "
                          "also the all-cores CPU baseline sample); 0 skips the check and the CPU baseline")
@@ -287,35 +290,52 @@ def main():
     fids = rank_frames(rank, world, W + K, F)
     epochs = sorted({f // 10 for f in fids})
     set_of = {e: i for i, e in enumerate(epochs)}
-    r = Renderer(wl.scene, Wd, H, max_frames=F, device=local, frames_per_launch=args.frames_per_launch)
+    NC = max(1, args.contexts)
+    ctxs = [Renderer(wl.scene, Wd, H, max_frames=F, device=local, frames_per_launch=args.frames_per_launch)
+            for _ in range(NC)]
+    r = ctxs[0]
     for e in epochs:
         st = wl.epoch(e)
-        r.set_instance_transforms(set_of[e], st.models)
-        if want_kp:
-            r.set_keypoints(set_of[e], st.keypoints)
-        if st.dr is not None:                      # C4: per-epoch lighting and texture DR
-            r.set_dr_light(set_of[e], st.dr.light)
-            r.set_dr_textures(set_of[e], st.dr.textures)
+        for c in ctxs:
+            c.set_instance_transforms(set_of[e], st.models)
+            if want_kp:
+                c.set_keypoints(set_of[e], st.keypoints)
+            if st.dr is not None:                      # C4: per-epoch lighting and texture DR
+                c.set_dr_light(set_of[e], st.dr.light)
+                c.set_dr_textures(set_of[e], st.dr.textures)
     views, projs = wl.frame_params(fids)
     frames = make_frames(views, projs, [set_of[f // 10] for f in fids], fids)
     frames_dev = torch.from_numpy(frames.view(np.uint8).copy()).to(dev)
     fsz = FRAME_DTYPE.itemsize
     Kp = r.n_kp
-    rgb = torch.empty((F, H, Wd, 3), dtype=torch.uint8, device=dev)
-    inst = torch.empty((F, H, Wd), dtype=torch.int32, device=dev)
-    dev_out = {"rgb": rgb, "instance": inst}
-    if "depth" in outs:
-        dev_out["depth"] = torch.empty((F, H, Wd), dtype=torch.float32, device=dev)
-    if "normals" in outs:
-        dev_out["normals"] = torch.empty((F, H, Wd, 3), dtype=torch.float16, device=dev)
-    if "points" in outs:
-        dev_out["points"] = torch.empty((F, H, Wd, 3), dtype=torch.float32, device=dev)
-    extra = {k: dev_out[k].data_ptr() for k in ("depth", "normals", "points") if k in dev_out}
-    if want_kp:
-        dev_out["keypoints_uv"] = torch.empty((F, Kp, 2), dtype=torch.float32, device=dev)
-        dev_out["keypoints_vis"] = torch.empty((F, Kp), dtype=torch.int32, device=dev)
-        extra.update(kp_uv=dev_out["keypoints_uv"].data_ptr(), kp_vis=dev_out["keypoints_vis"].data_ptr())
-    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def out_set():
+        d = {"rgb": torch.empty((F, H, Wd, 3), dtype=torch.uint8, device=dev),
+             "instance": torch.empty((F, H, Wd), dtype=torch.int32, device=dev)}
+        if "depth" in outs:
+            d["depth"] = torch.empty((F, H, Wd), dtype=torch.float32, device=dev)
+        if "normals" in outs:
+            d["normals"] = torch.empty((F, H, Wd, 3), dtype=torch.float16, device=dev)
+        if "points" in outs:
+            d["points"] = torch.empty((F, H, Wd, 3), dtype=torch.float32, device=dev)
+        if want_kp:
+            d["keypoints_uv"] = torch.empty((F, Kp, 2), dtype=torch.float32, device=dev)
+            d["keypoints_vis"] = torch.empty((F, Kp), dtype=torch.int32, device=dev)
+        return d
+    # one output set per context: consecutive steps on different contexts run
+    # concurrently, so they must not share output buffers
+    out_sets = [out_set() for _ in range(NC)]
+    dev_out = out_sets[0]
+    rgb, inst = dev_out["rgb"], dev_out["instance"]
+    extras = [{k: d[k].data_ptr() for k in ("depth", "normals", "points", "keypoints_uv", "keypoints_vis") if k in d}
+              for d in out_sets]
+    for x in extras:
+        for a, b in (("keypoints_uv", "kp_uv"), ("keypoints_vis", "kp_vis")):
+            if a in x:
+                x[b] = x.pop(a)
+    extra = extras[0]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NC - 1)]
+    stream = streams[0].cuda_stream
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s: {len(fids)} frames, {len(epochs)} epochs, "
         f"{wl.scene.n_tris_per_frame} tris/frame, K={Kp} keypoints")
 
@@ -323,27 +343,41 @@ def main():
         base = frames_dev.data_ptr() + s * F * fsz
         r.render_into(base, F, True, rgb.data_ptr(), inst.data_ptr(), stream=stream, **extra, **kw)
 
+    def timed_step(s):
+        # step s runs on context s % NC, into that context's outputs, on its stream
+        c = s % NC
+        base = frames_dev.data_ptr() + s * F * fsz
+        o = out_sets[c]
+        ctxs[c].render_into(base, F, True, o["rgb"].data_ptr(), o["instance"].data_ptr(),
+                            stream=streams[c].cuda_stream, **extras[c])
+
     for s in range(W):
-        step(s)
+        timed_step(s)
     torch.cuda.synchronize(dev)
-    r.synchronize()           # raises on any warm-up overflow (sticky flag), then clears it
-    r.timing_reset()
+    for c in ctxs:
+        c.synchronize()       # raises on any warm-up overflow (sticky flag), then clears it
+        c.timing_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for s in range(W, W + K):
-        step(s)
+        timed_step(s)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
     # The overflow flag is sticky across the asynchronous batches: this raises
     # (and no line is printed) if any timed batch truncated records or bins.
-    r.synchronize()
-    tm = r.timing_read()
-    bst = r.batch_stats()
+    tms, bsts = [], []
+    for c in ctxs:
+        c.synchronize()
+        tms.append(c.timing_read())
+        bsts.append(c.batch_stats())
+    tm = {k: sum(t[k] for t in tms) for k in tms[0]}
+    bst = {k: sum(b[k] for b in bsts) for k in bsts[0]}
     elapsed_max = max_over_ranks(elapsed, world)
+    dev_out = out_sets[(W + K - 1) % NC]        # the context that rendered the last timed step
 
     # ---- the last timed step's outputs, copied before anything reuses them --
     nver = args.verify_frames if world == 1 else min(args.verify_frames, args.verify_frames_multi)
@@ -501,6 +535,7 @@ def main():
                                    + (f" + {Kp} 2D keypoints/frame" if want_kp else "")
                                    + "".join(f" + {o}" for o in ("depth", "normals", "points") if o in outs),
                        "frames_per_step": F, "frames_per_launch": frames_per_launch, "seed": args.seed,
+                       "contexts": NC,
                        "width": Wd, "height": H, "tris_per_frame": wl.scene.n_tris_per_frame,
                        "parallelism": f"seed-sharded epochs x{world}, no collectives"},
             "roofline": rf,
