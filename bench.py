@@ -401,22 +401,34 @@ def main():
     value = aggregate_value(K, F, world, elapsed_max)
     traffic = None
     valu = None
+    work = None
     if os.path.exists(args.profile_json):
         try:
             pj = json.load(open(args.profile_json))
             if (pj.get("workload") == args.workload and pj.get("frames_per_launch") == frames_per_launch
                     and pj.get("B_frame") == b_geom + b_tex + b_out):
                 traffic = {k: v for k, v in pj.get("bytes_per_launch", {}).items()}
+                work = pj.get("k_raster_work_per_frame")
                 if pj.get("k_raster_valu_busy") is not None:
                     valu = {"busy": round(pj["k_raster_valu_busy"], 3),
                             "lane_util": round(pj.get("k_raster_valu_lane_util") or 0.0, 3),
                             "note": "k_raster's limiter: VALU issue (rocprofv3 SQ_ACTIVE_INST_VALU, "
                                     "profiles/pmc_traffic.json)"}
         except Exception:
-            traffic = valu = None
+            traffic = valu = work = None
     rf = roofline(b_geom, b_tex, b_out, frames_per_launch, tm["ms_raster"] / launches, tm["ms_setup"] / launches,
                   bst["records"] / max(bst["frames"], 1), value / world, traffic)
     rf["valu"] = valu
+    # work rates (a tris/s and fragments/s figure beside the bytes)
+    fps_gpu = value / world
+    rates = {"tris_per_s": round(fps_gpu * wl.scene.n_tris_per_frame),
+             "raster_records_per_s": round(fps_gpu * bst["records"] / max(bst["frames"], 1)),
+             "bin_entries_per_s": round(fps_gpu * bst["bin_entries"] / max(bst["frames"], 1)),
+             "per": "GPU"}
+    if work is not None:
+        rates["fragments_per_s"] = round(fps_gpu * work["fragments"])
+        rates["fragments_note"] = work.get("source")
+    rf["rates"] = rates
     if traffic is not None:
         rf["traffic_note"] = ("HBM bytes per launch from rocprofv3 PMC: FETCH_SIZE x 2 (gfx950 counts half of a "
                               "128-B read request, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, KB = 1024 B")
