@@ -655,9 +655,17 @@ __device__ __forceinline__ int find_bin_item(const uint32_t* pre, uint32_t j) {
 }
 
 // Load this thread's records of the round at `base` (record ids base + tid*kBinRpt + q),
-// fill lrc[] and pre[]; returns the round's item total.
+// fill lrc[] and pre[]; returns the round's item total.  With kSingle, a
+// record touching at most kCountDirect tiles (most of them) is not expanded:
+// its own thread calls `single(q, tile)` for each tile.  k_count does so (its
+// counts do not depend on the order; C3: binning 0.64 -> 0.52 ms, frames/s
+// +0.8%); k_bin expands every record, so a tile's list keeps the record order
+// the raster is tuned for (binning single-tile records directly in k_bin too
+// saved 0.07 ms there and cost 0.06 ms of raster).
+constexpr uint32_t kCountDirect = 4;
+template <bool kSingle, typename Single>
 __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32_t base, uint32_t n, uint32_t* lrc,
-                                                    uint32_t* pre, uint32_t* wsum) {
+                                                    uint32_t* pre, uint32_t* wsum, uint32_t tiles_x, Single single) {
   const int tid = threadIdx.x;
   const uint32_t r0 = base + (uint32_t)tid * kBinRpt;
   uint32_t rc[kBinRpt], area[kBinRpt], sum = 0;
@@ -675,6 +683,11 @@ __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32
   for (int q = 0; q < kBinRpt; ++q) {
     area[q] = (r0 + (uint32_t)q < n) ? rect_area(rc[q]) : 0u;
     lrc[tid * kBinRpt + q] = rc[q];
+    if (kSingle && area[q] && area[q] <= kCountDirect) {
+#pragma clang loop unroll(disable)
+      for (uint32_t a = 0; a < area[q]; ++a) single(q, rect_tile(rc[q], a, tiles_x));
+      area[q] = 0u;
+    }
   }
 #pragma unroll
   for (int q = 0; q < kBinRpt; ++q) sum += area[q];
@@ -705,7 +718,8 @@ __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-    const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
+    const uint32_t total = bin_round_setup<true>(rect, base, n, lrc, pre, wsum, s.tiles_x,
+                                                 [&](int, uint32_t t) { atomicAdd(&hist[t], 1u); });
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
       const int k = find_bin_item(pre, j);
@@ -792,7 +806,7 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
     hist[t] = toff[t] + tcnt[t] - bo[t] - 1u;   // last slot of the mirrored range; decremented
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-    const uint32_t total = bin_round_setup(rect, base, n, lrc, pre, wsum);
+    const uint32_t total = bin_round_setup<false>(rect, base, n, lrc, pre, wsum, s.tiles_x, [](int, uint32_t) {});
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
       const int k = find_bin_item(pre, j);
