@@ -660,10 +660,10 @@ __device__ __forceinline__ int find_bin_item(const uint32_t* pre, uint32_t j) {
 // its own thread calls `single(q, tile)` for each tile.  k_count does so (its
 // counts do not depend on the order; C3: binning 0.64 -> 0.52 ms, frames/s
 // +0.8%); k_bin expands every record, so a tile's list keeps the record order
-// the raster is tuned for (binning single-tile records directly in k_bin too
-// saved 0.07 ms there and cost 0.06 ms of raster).
+// the raster is tuned for (binning single-tile records directly in k_bin too,
+// in or out of record order, saved at most 0.07 ms there and cost as much raster).
 constexpr uint32_t kCountDirect = 4;
-template <bool kSingle, typename Single>
+template <uint32_t kDirect, typename Single>
 __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32_t base, uint32_t n, uint32_t* lrc,
                                                     uint32_t* pre, uint32_t* wsum, uint32_t tiles_x, Single single) {
   const int tid = threadIdx.x;
@@ -683,7 +683,7 @@ __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32
   for (int q = 0; q < kBinRpt; ++q) {
     area[q] = (r0 + (uint32_t)q < n) ? rect_area(rc[q]) : 0u;
     lrc[tid * kBinRpt + q] = rc[q];
-    if (kSingle && area[q] && area[q] <= kCountDirect) {
+    if (kDirect && area[q] && area[q] <= kDirect) {
 #pragma clang loop unroll(disable)
       for (uint32_t a = 0; a < area[q]; ++a) single(q, rect_tile(rc[q], a, tiles_x));
       area[q] = 0u;
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-    const uint32_t total = bin_round_setup<true>(rect, base, n, lrc, pre, wsum, s.tiles_x,
+    const uint32_t total = bin_round_setup<kCountDirect>(rect, base, n, lrc, pre, wsum, s.tiles_x,
                                                  [&](int, uint32_t t) { atomicAdd(&hist[t], 1u); });
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
@@ -806,7 +806,7 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
     hist[t] = toff[t] + tcnt[t] - bo[t] - 1u;   // last slot of the mirrored range; decremented
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-    const uint32_t total = bin_round_setup<false>(rect, base, n, lrc, pre, wsum, s.tiles_x, [](int, uint32_t) {});
+    const uint32_t total = bin_round_setup<0>(rect, base, n, lrc, pre, wsum, s.tiles_x, [](int, uint32_t) {});
     __syncthreads();
     for (uint32_t j = tid; j < total; j += kBlock) {
       const int k = find_bin_item(pre, j);
