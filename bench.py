@@ -48,7 +48,11 @@ sys.path.insert(0, ROOT)
 METRIC = "annotated frames/sec (RGB+seg+2D kpts) at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 RECORD_BYTES = 80 + 4  # k_setup writes one 80-B raster record + its 4-B tile rectangle per record
-DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 240
+# 1,600 frames per step = one launch chain: the kernels' ramp-down and the short
+# kernels' fixed cost are paid once per launch (C3, frames/s: 240 -> 22.09k,
+# 480 -> 22.20k, 960 -> 22.52k, 1,920 -> 22.73k; profiles/r03/ab/frames_per_step.txt);
+# 23 steps x 1,600 frames = 3,680 epochs stay below the library's 4,096 transform sets
+DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 1600
 
 
 def log(*a):

@@ -2,7 +2,7 @@
 
 * C3 exactly as bench.py times it: 1920x1080, world2 + crane/dumper/human
   proxies, 2D keypoints, seed 0, frames drawn from the bench's timed steps
-  (warm-up 3, steps 20, 240 frames per step) -- bit-exact.
+  (warm-up 3, steps 20, bench.DEFAULT_FRAMES_PER_STEP frames per step) -- bit-exact.
 * C2: 32 frames sampled across the scheduled 1,000-pose sequence of world2
   static (BASELINE configs[1]: 1920x1080, randomised camera poses) --
   bit-exact.

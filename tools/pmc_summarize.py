@@ -74,7 +74,14 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
                 "k_raster_valu_busy": out["k_raster"].get("valu_busy"),
                 "k_raster_valu_lane_util": out["k_raster"].get("valu_lane_util"),
                 "source": os.path.basename(os.path.normpath(root))}
-        json.dump(prof, open(os.path.join(here, "profiles", "pmc_traffic.json"), "w"), indent=1)
+        path = os.path.join(here, "profiles", "pmc_traffic.json")
+        try:   # per-frame work counts (profiling counters) do not depend on the launch size: keep them
+            keep = json.load(open(path)).get("k_raster_work_per_frame")
+            if keep:
+                prof["k_raster_work_per_frame"] = keep
+        except Exception:
+            pass
+        json.dump(prof, open(path, "w"), indent=1)
 
 
 if __name__ == "__main__":
