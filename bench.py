@@ -48,11 +48,13 @@ sys.path.insert(0, ROOT)
 METRIC = "annotated frames/sec (RGB+seg+2D kpts) at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 RECORD_BYTES = 80 + 4  # k_setup writes one 80-B raster record + its 4-B tile rectangle per record
-# 1,600 frames per step = one launch chain: the kernels' ramp-down and the short
+# 960 frames per step = one launch chain: the kernels' ramp-down and the short
 # kernels' fixed cost are paid once per launch (C3, frames/s: 240 -> 22.09k,
-# 480 -> 22.20k, 960 -> 22.52k, 1,920 -> 22.73k; profiles/r03/ab/frames_per_step.txt);
-# 23 steps x 1,600 frames = 3,680 epochs stay below the library's 4,096 transform sets
-DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 1600
+# 480 -> 22.20k, 960 -> 22.51k, 1,600 -> 22.60k, 1,920 -> 22.73k;
+# profiles/r03/ab/frames_per_step.txt).  960 keeps a rank's work buffers near
+# 100 GB (the library sizes them for every triangle of every frame), so two
+# ranks still share one MI355X in a rehearsal
+DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 960
 
 
 def log(*a):
@@ -271,7 +273,19 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
+        # Gloo's C++ side prints its connection report ("[Gloo] Rank r is connected
+        # to ...") on stdout while the mesh forms; stdout carries only the JSON line,
+        # so the descriptor points at stderr until the first barrier has completed
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", init_method="env://")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     from constructionsceneposeestimation_amd.renderer import FRAME_DTYPE, Renderer, make_frames
     from constructionsceneposeestimation_amd.workload import WORKLOADS, Workload
