@@ -55,6 +55,14 @@ RECORD_BYTES = 80 + 4  # k_setup writes one 80-B raster record + its 4-B tile re
 # 100 GB (the library sizes them for every triangle of every frame), so two
 # ranks still share one MI355X in a rehearsal
 DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 960
+# Larger frames (C5 at 3840x2160 with depth, normals and points: ~200 MB of
+# outputs per frame) keep the round-2 step of 240 frames, so a rank stays
+# within one GPU's 288 GB.
+LARGE_FRAME_PIXELS, LARGE_FRAMES_PER_STEP = 1920 * 1080, 240
+
+
+def default_frames_per_step(width: int, height: int) -> int:
+    return DEFAULT_FRAMES_PER_STEP if width * height <= LARGE_FRAME_PIXELS else LARGE_FRAMES_PER_STEP
 
 
 def log(*a):
@@ -246,7 +254,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=DEFAULT_STEPS)
     ap.add_argument("--warmup", type=int, default=DEFAULT_WARMUP)
-    ap.add_argument("--frames-per-step", type=int, default=DEFAULT_FRAMES_PER_STEP)
+    ap.add_argument("--frames-per-step", type=int, default=0,
+                    help=f"frames per step = per launch chain (0: {DEFAULT_FRAMES_PER_STEP}, or "
+                         f"{LARGE_FRAMES_PER_STEP} above 1920x1080)")
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--frames-per-launch", type=int, default=0, help="frames per kernel chain (0 = library default)")
     ap.add_argument("--seed", type=int, default=0)
@@ -296,10 +306,10 @@ def main():
     local = local % ndev if ndev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    F = args.frames_per_step
     K, W = args.steps, args.warmup
     wl = Workload(args.workload, seed=args.seed)
     H, Wd = wl.height, wl.width
+    F = args.frames_per_step or default_frames_per_step(Wd, H)
     outs = set(WORKLOADS[args.workload]["outputs"])   # C5 adds depth, normals and world points
     want_kp = "keypoints" in outs
     t0 = time.time()

@@ -99,3 +99,8 @@ def test_elapsed_is_max_and_counts_sum_over_ranks_gloo(tmp_path):
     mp.spawn(_rank_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     got, tot = eval(open(out).read())
     assert got == 1.5 and tot == [8, 1]
+
+
+def test_default_frames_per_step_by_frame_size():
+    assert bench.default_frames_per_step(1920, 1080) == bench.DEFAULT_FRAMES_PER_STEP
+    assert bench.default_frames_per_step(3840, 2160) == bench.LARGE_FRAMES_PER_STEP < bench.DEFAULT_FRAMES_PER_STEP
