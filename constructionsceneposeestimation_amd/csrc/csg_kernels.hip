@@ -227,7 +227,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// exclusive scan over the 256-thread block; `wsum` is LDS[4]
+// exclusive scan over the 256-thread block; `wsum` is LDS[4].  kTrail = false
+// skips the closing barrier: for a `wsum` whose next scan is already ordered
+// after this one's reads by some other barrier.
+template <bool kTrail = true>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
   const uint32_t inc = wave_incl_scan(v);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -240,7 +243,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
     off += (k < w) ? x : 0u;
     tot += x;
   }
-  __syncthreads();
+  if (kTrail) __syncthreads();
   total = tot;
   return off + inc - v;
 }
@@ -1128,7 +1131,8 @@ struct RasterLds {
   uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
   uint32_t starts[kBlock];              // bit i: a span starts at level-2 item i (<= 256 spans x 32 px)
   uint16_t before[kBlock + 1];          // spans starting before item 32*d
-  uint32_t wsum[kBlock / 64];
+  uint32_t wsum[kBlock / 64];           // the batch scan's wave totals
+  uint32_t wsum2[kBlock / 64];          // the level-2 scan's (each reused only after other barriers)
 };
 
 // Block-level two-level expansion of kStage-record batches.
@@ -1169,7 +1173,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
     if (tid < NS) L.starts1[tid] = 0u;   // ordered before the atomics by the scan's barriers
     if (tid == 0) L.before1[0] = 0;
     uint32_t tot1p;
-    const uint32_t ex1p = block_excl_scan(rows | (rows ? 0x10000u : 0u), L.wsum, tot1p);
+    const uint32_t ex1p = block_excl_scan<false>(rows | (rows ? 0x10000u : 0u), L.wsum, tot1p);
     const uint32_t tot1 = tot1p & 0xFFFFu;
     if (rows) {
       const uint32_t ex1 = ex1p & 0xFFFFu, ci = ex1p >> 16, e_end = ex1 + rows;
@@ -1220,7 +1224,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
       L.starts[tid] = 0u;                 // ordered before the atomics by the scan's barriers
       if (tid == 0) L.before[0] = 0;
       uint32_t totp;
-      const uint32_t exp = block_excl_scan(w2 | (w2 ? 0x10000u : 0u), L.wsum, totp);
+      const uint32_t exp = block_excl_scan<false>(w2 | (w2 ? 0x10000u : 0u), L.wsum2, totp);
       const uint32_t ex2 = exp & 0xFFFFu, tot2 = totp & 0xFFFFu;
       if (w2) {
         const uint32_t ci = exp >> 16, e_end = ex2 + w2;
