@@ -1462,6 +1462,21 @@ __device__ __forceinline__ bool swizzled_tile(uint32_t v, uint32_t tiles_x, uint
   return true;
 }
 
+// Output stores of 4 consecutive pixels (a thread's quarter of a tile row).
+// ids: 16 B, and 8 threads write a tile row's ids as one aligned 128-B line,
+// stored non-temporally (kept out of L2, where records and textures are
+// re-read; C3: raster -0.2%, profiles/r03/ab/output_stores.txt); RGB8: 12 B as
+// one 3-dword store (4-B aligned: the pixel index is a multiple of 4; its
+// 96-B row segments are not whole lines, so they stay ordinary stores).
+typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void out_ids(int32_t* p, int4 v) {
+  const v4i32 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<v4i32*>(p));
+}
+__device__ __forceinline__ void out_rgb4(uint8_t* p, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+  *reinterpret_cast<uint3*>(p) = make_uint3(c0 | (c1 << 24), (c1 >> 8) | (c2 << 16), (c2 >> 16) | (c3 << 8));
+}
+
 // A tile without bin entries: every pixel is background (sky, id -1, depth
 // +inf, normal 0, point NaN) and every in-tile keypoint is visible (its W is
 // compared with +inf, as in the general path).  No z-buffer, table or barrier.
@@ -1484,13 +1499,8 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
   const uint32_t sky = b.lights[b.fset[f]].sky & 0xFFFFFFu;
   const float nan = __builtin_nanf("");
   if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
-    if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(-1, -1, -1, -1);
-    if (b.rgb) {
-      uint32_t* d = reinterpret_cast<uint32_t*>(b.rgb + o * 3);
-      d[0] = sky | (sky << 24);
-      d[1] = (sky >> 8) | (sky << 16);
-      d[2] = (sky >> 16) | (sky << 8);
-    }
+    if (b.inst) out_ids(b.inst + o, make_int4(-1, -1, -1, -1));
+    if (b.rgb) out_rgb4(b.rgb + o * 3, sky, sky, sky, sky);
     if (b.depth) *reinterpret_cast<float4*>(b.depth + o) = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
     if (b.normals) {
       uint2* d = reinterpret_cast<uint2*>(b.normals + o * 3);
@@ -1805,13 +1815,8 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       ids[k] = (int32_t)(w >> 32);
     }
     if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
-      if (b.inst) *reinterpret_cast<int4*>(b.inst + o) = make_int4(ids[0], ids[1], ids[2], ids[3]);
-      if (b.rgb) {
-        uint32_t* d = reinterpret_cast<uint32_t*>(b.rgb + o * 3);
-        d[0] = rgb[0] | (rgb[1] << 24);
-        d[1] = (rgb[1] >> 8) | (rgb[2] << 16);
-        d[2] = (rgb[2] >> 16) | (rgb[3] << 8);
-      }
+      if (b.inst) out_ids(b.inst + o, make_int4(ids[0], ids[1], ids[2], ids[3]));
+      if (b.rgb) out_rgb4(b.rgb + o * 3, rgb[0], rgb[1], rgb[2], rgb[3]);
     } else {
       for (int k = 0; k < 4 && px0 + k < (int)s.W; ++k) {
         if (b.inst) b.inst[o + k] = ids[k];
