@@ -434,6 +434,7 @@ __device__ __forceinline__ uint32_t rect_tile(uint32_t rc, uint32_t q, uint32_t 
   return __umul24(ty0 + r, tiles_x) + tx0 + (q - __umul24(r, w));
 }
 
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 // Grid: x = frame (fast), (y, z) = chunk.  Consecutive workgroups take the
 // same chunk for successive frames, so a chunk's triangles (and its clip
 // rows' instance) are read from HBM once and then hit in L2 (measured on C3:
@@ -601,7 +602,11 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   // [wbase, wbase + wtot), but lane-by-lane 16-B stores at an 80-B stride
   // write many more partial 128-B lines than the bytes need.  So, 16 records
   // at a time, the lanes holding them put them in a per-wave LDS stage and the
-  // wave stores the stage as consecutive 16-B chunks (1 KB per instruction).
+  // wave stores the stage as consecutive 16-B chunks (1 KB per instruction),
+  // non-temporally: whole lines that would otherwise push the chunk's
+  // triangles, which the next frames' workgroups re-read, out of L2 (setup
+  // -1.1%, profiles/r03/ab/nt_record_stores.txt; round 1's non-temporal stores
+  // of scattered 112-B records were 5x slower: partial lines).
   // Wave-local: the loop count is uniform per wave, so there is no block barrier.
   static_assert(16 * kRecGroups <= 2 * 64, "two chunk stores per lane");
   __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
@@ -626,7 +631,11 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     const size_t at = ((size_t)wbase + p0) * kRecGroups;
 #pragma unroll
     for (uint32_t c = (uint32_t)lane; c < 2u * 64u; c += 64u)
-      if (c < nch && at + c < lim) dst[at + c] = sw[c];
+      if (c < nch && at + c < lim) {   // non-temporal: k_raster reads them long after L2 has turned over
+        const uint4 q = sw[c];
+        const v4u32 w = {q.x, q.y, q.z, q.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<v4u32*>(dst + at + c));
+      }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
