@@ -119,6 +119,21 @@ def sum_over_ranks(vals: List[int], world: int) -> List[int]:
     return [int(v) for v in t.tolist()]
 
 
+def shard_report(timed: List[int], world: int) -> dict:
+    """Each rank's timed frame ids gathered on every rank (gloo): the seed
+    shards must be disjoint, and their union is what ``value`` counts."""
+    lists = [list(timed)]
+    if world > 1:
+        import torch.distributed as dist
+        lists = [None] * world
+        dist.all_gather_object(lists, list(timed))
+    sets = [set(x) for x in lists]
+    union = set().union(*sets)
+    return {"ranks": world, "timed_frames_per_rank": [len(x) for x in lists],
+            "union": len(union), "disjoint": len(union) == sum(len(x) for x in lists),
+            "epochs_mod_world": [sorted({(f // 10) % world for f in x}) for x in lists]}
+
+
 def median_time(fn: Callable[[], None], runs: int = 5, warmup: int = 1, what: str = "") -> float:
     """Median wall time of ``runs`` calls after ``warmup`` untimed ones.
     A progress line per call (stderr): a long CPU baseline is not silent."""
@@ -271,6 +286,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU run (0 = all available)")
     ap.add_argument("--pcie-steps", type=int, default=3, help="batches timed with host outputs (0 = skip)")
     ap.add_argument("--stats-steps", type=int, default=5, help="batches timed with label statistics (0 = skip)")
+    ap.add_argument("--size-work", type=int, default=1,
+                    help="1: size the work buffers by a sizing pass over the schedule (csg_size_work); "
+                         "0: the library's full-scene caps")
+    ap.add_argument("--work-margin", type=float, default=0.25, help="cap = largest measured count x (1 + margin)")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -336,6 +355,17 @@ def main():
     frames_dev = torch.from_numpy(frames.view(np.uint8).copy()).to(dev)
     fsz = FRAME_DTYPE.itemsize
     Kp = r.n_kp
+    # Work buffers sized by a sizing pass over this rank's whole schedule (setup
+    # and binning kernels only, outside the timed region): caps = the largest
+    # per-frame record / bin-entry counts x 1.25, so no batch can overflow
+    # (the counts are a pure function of the frame); without it the library
+    # sizes them for every scene triangle per frame (~100 GB at C3 x 960 frames)
+    winfo = None
+    if args.size_work:
+        for c in ctxs:
+            winfo = c.size_work(frames_dev.data_ptr(), len(fids), on_device=True, margin=args.work_margin)
+    else:
+        winfo = r.work_info()
 
     def out_set():
         d = {"rgb": torch.empty((F, H, Wd, 3), dtype=torch.uint8, device=dev),
@@ -447,6 +477,14 @@ def main():
     rf = roofline(b_geom, b_tex, b_out, frames_per_launch, tm["ms_raster"] / launches, tm["ms_setup"] / launches,
                   bst["records"] / max(bst["frames"], 1), value / world, traffic)
     rf["valu"] = valu
+    if NC > 1:
+        # steps on different contexts run at the same time, so each stream's
+        # event interval includes time spent sharing the GPU with the other
+        # context: no per-kernel time (the frame-level figure stands)
+        rf["kernels"] = []
+        rf["avg_launch_ms"] = None
+        rf["kernels_note"] = (f"{NC} contexts overlap on the GPU: per-kernel HIP-event times are not kernel times; "
+                              "time kernels with --contexts 1")
     # work rates (a tris/s and fragments/s figure beside the bytes)
     fps_gpu = value / world
     rates = {"tris_per_s": round(fps_gpu * wl.scene.n_tris_per_frame),
@@ -496,6 +534,7 @@ def main():
             v_, p_, ref = ver.render(sample_frames, 2)
             bad = ver.compare(sample_frames, v_, p_, ref, gpu_sample)
     n_checked, n_bad = sum_over_ranks([len(sample_frames), len(bad)], world)
+    shards = shard_report(timed_frames(fids, W, K, F), world)
     if n_bad:
         for b in bad[:20]:
             log(f"[rank {rank}] VERIFY FAILED: {b}")
@@ -584,9 +623,19 @@ def main():
                          "outputs": sorted(gpu_sample) if gpu_sample else [],
                          "against": "oracle/csg_oracle.c on frames of the last timed step",
                          "overflow": "none: sticky flag checked after the warm-up and after the timed steps"},
+            "shards": shards,
             "pcie_inclusive": pcie,
             "with_label_stats": with_stats,
             "stage_ms_per_step": {k: round(tm[k] / K, 4) for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")},
+            "work": {"bytes": int(winfo["work_bytes"]), "contexts": NC,
+                     "records_per_frame_cap": int(winfo["records_per_frame"]),
+                     "bins_per_frame_cap": int(winfo["bins_per_frame"]),
+                     "frames_per_launch": int(winfo["frames_per_launch"]),
+                     "sized_frames": int(winfo["sized_frames"]), "max_records": int(winfo["max_records"]),
+                     "max_bins": int(winfo["max_bins"]), "mean_records": round(winfo["mean_records"], 1),
+                     "mean_bins": round(winfo["mean_bins"], 1),
+                     "how": (f"csg_size_work over the rank's {len(fids)} scheduled frames, margin {args.work_margin}"
+                             if args.size_work else "full-scene caps (1.125 x triangles per frame)")},
             "records_per_frame": round(bst["records"] / max(bst["frames"], 1), 1),
             "bin_entries_per_frame": round(bst["bin_entries"] / max(bst["frames"], 1), 1),
         }

@@ -12,7 +12,7 @@ from typing import Optional
 PKG = os.path.dirname(os.path.abspath(__file__))
 # CSG_LIB names an alternative build of the same ABI (A/B timing of kernel variants)
 LIB_PATH = os.environ.get("CSG_LIB") or os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 8  # CSG_ABI_VERSION in include/csg_api.h
+ABI_VERSION = 9  # CSG_ABI_VERSION in include/csg_api.h
 KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
 COVERED_UNKNOWN = 0x80000000  # csg_outputs.label_covered flag: a tile held more than 32 labels
 ERR_CAPACITY = -6  # CSG_ERR_CAPACITY
@@ -24,7 +24,8 @@ EXPORTED = (
     "csg_upload_texture", "csg_set_light", "csg_set_instance_transforms", "csg_set_keypoints",
     "csg_render_batch", "csg_render_batch_async", "csg_synchronize", "csg_get_batch_stats",
     "csg_project_keypoints", "csg_timing_reset", "csg_timing_read", "csg_set_dr_light", "csg_set_dr_textures",
-    "csg_instance_bounds", "csg_copy_files", "csg_host_alloc", "csg_host_free",
+    "csg_instance_bounds", "csg_copy_files", "csg_host_alloc", "csg_host_free", "csg_size_work",
+    "csg_get_work_info",
 )
 
 
@@ -85,6 +86,13 @@ class BatchStats(C.Structure):
 class Timing(C.Structure):
     _fields_ = [("batches", C.c_uint32), ("frames", C.c_uint32), ("ms_setup", C.c_double),
                 ("ms_bin", C.c_double), ("ms_raster", C.c_double), ("ms_keypoints", C.c_double)]
+
+
+class WorkInfo(C.Structure):
+    _fields_ = [("records_per_frame", C.c_uint32), ("bins_per_frame", C.c_uint32),
+                ("frames_per_launch", C.c_uint32), ("sized_frames", C.c_uint32), ("max_records", C.c_uint32),
+                ("max_bins", C.c_uint32), ("mean_records", C.c_double), ("mean_bins", C.c_double),
+                ("work_bytes", C.c_uint64)]
 
 
 _lib: Optional[C.CDLL] = None
@@ -149,6 +157,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib.csg_set_dr_light.argtypes = [vp, u32, C.POINTER(Light)]
     lib.csg_set_dr_textures.argtypes = [vp, u32, vp, u32]
     lib.csg_instance_bounds.argtypes = [vp, u32, vp]
+    lib.csg_size_work.argtypes = [vp, vp, u32, i32, C.c_float, C.POINTER(WorkInfo)]
+    lib.csg_get_work_info.argtypes = [vp, C.POINTER(WorkInfo)]
     if lib.csg_abi_version() != ABI_VERSION:
         raise CsgError(f"libcsg.so ABI {lib.csg_abi_version()} != binding ABI {ABI_VERSION}; rebuild")
     _lib = lib

@@ -38,19 +38,6 @@ SUPPORTED = ("rgb", "distance_to_image_plane", "instance_segmentation", "boundin
 _NEEDS = {"pointcloud": ("points",), "normals": ("normals",), "bounding_box_3d": ("covered",)}
 
 
-def unproject_depth(depth: np.ndarray, cam_to_world: np.ndarray, intr) -> np.ndarray:
-    """World coordinates of every pixel centre with finite depth (USD camera
-    convention: X right, Y up, looking along -Z)."""
-    H, W = depth.shape
-    vv, uu = np.mgrid[0:H, 0:W]
-    m = np.isfinite(depth)
-    d = depth[m].astype(np.float64)
-    xc = (uu[m] + 0.5 - intr.cx) * d / intr.fx
-    yc = -(vv[m] + 0.5 - intr.cy) * d / intr.fy
-    pc = np.stack([xc, yc, -d], 1)
-    return (pc @ cam_to_world[:3, :3].T + cam_to_world[:3, 3]).astype(np.float32), m
-
-
 class Annotator:
     def __init__(self, name: str):
         if name not in SUPPORTED:

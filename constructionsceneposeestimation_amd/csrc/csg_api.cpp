@@ -169,6 +169,9 @@ struct csg_ctx {
   uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
   uint32_t bin_blocks = 32;             // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only)
   uint32_t chain_frames = 0;            // frames per launch chain (cfg.frames_per_launch; CSG_CHAIN overrides)
+  // the last sizing pass (csg_size_work)
+  uint32_t sized_frames = 0, sized_max_rec = 0, sized_max_bin = 0;
+  double sized_mean_rec = 0.0, sized_mean_bin = 0.0;
 
   int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -694,6 +697,28 @@ static int sync_scene_state(csg_ctx* c) {
   return CSG_OK;
 }
 
+// Record cap no frame can exceed: every triangle, plus 1/8 for the second
+// triangle of near-plane clips (and slack), rounded to 16-B rect rows.
+static uint32_t full_record_cap(const csg_ctx* c) {
+  const uint64_t n = std::min<uint64_t>(c->n_tris_total + c->n_tris_total / 8 + 4096, 0x7FFFFFF0ull);
+  return (uint32_t)((n + 3u) & ~3ull);
+}
+
+// Device bytes ensure_work allocates for a launch chain of F frames at the given caps.
+static uint64_t work_bytes_for(const csg_ctx* c, uint64_t F, uint64_t rec_cap, uint64_t bin_cap) {
+  const uint64_t per_frame = rec_cap * (sizeof(Rec) + 4) + bin_cap * 4 +
+                             (uint64_t)c->n_tiles * 4 * (2 + c->bin_blocks) + 4 + (uint64_t)c->n_inst * 12 * 4 +
+                             12 * 4 + kCamFloats * 4 + kCounterStride * 4 + 4;
+  return F * per_frame + (uint64_t)c->cfg.max_frames * sizeof(FrameDev);
+}
+
+static void release_work(csg_ctx* c) {
+  c->recs.release(); c->rect.release(); c->bins.release(); c->bcount.release();
+  c->tile_count.release(); c->tile_off.release(); c->rec_count.release();
+  c->clip.release(); c->pv.release(); c->cam.release(); c->fset.release();
+  c->work_frames = 0;
+}
+
 static int ensure_work(csg_ctx* c) {
   const uint32_t maxF = c->chain_frames;   // work buffers hold one launch chain
   if (c->work_frames == maxF && c->rec_cap && c->bin_cap) return CSG_OK;
@@ -701,10 +726,7 @@ static int ensure_work(csg_ctx* c) {
     const int rc = drain(c);
     if (rc) return rc;
   }
-  if (!c->rec_cap)
-    c->rec_cap = c->cfg.records_per_frame ? c->cfg.records_per_frame
-                                          : (uint32_t)std::min<uint64_t>(c->n_tris_total + c->n_tris_total / 8 + 4096,
-                                                                         0x7FFFFFFFull);
+  if (!c->rec_cap) c->rec_cap = c->cfg.records_per_frame ? c->cfg.records_per_frame : full_record_cap(c);
   c->rec_cap = (c->rec_cap + 3u) & ~3u;   // 16-B aligned rect rows per frame (k_count / k_bin load 4 at once)
   if (!c->bin_cap)
     c->bin_cap = c->cfg.bins_per_frame ? c->cfg.bins_per_frame
@@ -1198,6 +1220,170 @@ int csg_timing_read(csg_ctx* c, csg_timing* out) {
     out->frames += c->ring_frames[k];
   }
   out->batches = (uint32_t)n;
+  return CSG_OK;
+}
+
+// Sizing pass: k_clip, k_setup, k_count, k_colscan and k_scan over the
+// frames in chains of kProbeFrames, with a record cap no frame can exceed
+// and no bin cap (k_bin is not run); per frame the record count (k_setup's
+// counter, which counts past the cap) and the bin total (tile_off[n_tiles]).
+static int measure_work(csg_ctx* c, const csg_frame* frames, uint32_t n, bool on_device, std::vector<uint32_t>& recs_n,
+                        std::vector<uint32_t>& bins_n) {
+  constexpr uint32_t kProbeFrames = 64;
+  const uint32_t P = std::min(kProbeFrames, n);
+  uint32_t cap = full_record_cap(c);
+  recs_n.assign(n, 0);
+  bins_n.assign(n, 0);
+  DevBuf<FrameDev> hframes;
+  if (!on_device) HIP_TRY(c, hframes.alloc(P));
+  SceneDev s = scene_dev(c);
+  hipStream_t st = c->stream;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    release_work(c);
+    HIP_TRY(c, c->fset.alloc(P));
+    HIP_TRY(c, c->clip.alloc((size_t)P * c->n_inst * 12));
+    HIP_TRY(c, c->pv.alloc((size_t)P * 12));
+    HIP_TRY(c, c->cam.alloc((size_t)P * kCamFloats));
+    HIP_TRY(c, c->recs.alloc((size_t)P * cap));
+    HIP_TRY(c, c->rect.alloc((size_t)P * cap));
+    HIP_TRY(c, c->rec_count.alloc((size_t)P * kCounterStride));
+    HIP_TRY(c, c->tile_count.alloc((size_t)P * c->n_tiles));
+    HIP_TRY(c, c->tile_off.alloc((size_t)P * (c->n_tiles + 1)));
+    HIP_TRY(c, c->bcount.alloc((size_t)P * c->bin_blocks * c->n_tiles));
+    uint32_t worst = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += P) {
+      const uint32_t Fc = std::min(P, n - c0);
+      const FrameDev* df;
+      if (on_device) {
+        df = reinterpret_cast<const FrameDev*>(frames) + c0;
+      } else {
+        HIP_TRY(c, hipMemcpy(hframes.p, frames + c0, sizeof(FrameDev) * Fc, hipMemcpyHostToDevice));
+        df = hframes.p;
+      }
+      BatchDev b{};
+      b.frames = df;
+      b.fset = c->fset.p;
+      b.n_sets = (uint32_t)c->set_valid.size();
+      b.n_kp_sets = (uint32_t)c->kp_valid.size();
+      b.models = c->models.p;
+      b.mats = c->set_mats.p;
+      b.iset = c->iset.p;
+      b.lights = c->lights.p;
+      b.n_mat = c->n_materials;
+      b.clip = c->clip.p;
+      b.pv = c->pv.p;
+      b.cam = c->cam.p;
+      b.recs = c->recs.p;
+      b.rect = c->rect.p;
+      b.rec_cap = cap;
+      b.rec_count = c->rec_count.p;
+      b.tile_count = c->tile_count.p;
+      b.bcount = c->bcount.p;
+      b.bin_blocks = c->bin_blocks;
+      b.tile_off = c->tile_off.p;
+      b.bin_cap = 0x7FFFFFFFu;
+      b.overflow = c->overflow.p;
+      b.dbg = c->dbg;
+      b.tile_words = (c->n_tiles + 31u) / 32u;
+      HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * Fc * kCounterStride, st));
+      launch_clip(s, b, Fc, st);
+      launch_setup(s, b, c->chunks.p, c->n_chunks, Fc, st);
+      launch_count(s, b, Fc, c->bin_blocks, st);
+      launch_colscan(s, b, Fc, st);
+      launch_scan(s, b, Fc, st);
+      HIP_TRY(c, hipGetLastError());
+      HIP_TRY(c, hipMemcpy2DAsync(recs_n.data() + c0, 4, c->rec_count.p, kCounterStride * 4, 4, Fc,
+                                  hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipMemcpy2DAsync(bins_n.data() + c0, 4, c->tile_off.p + c->n_tiles, (size_t)(c->n_tiles + 1) * 4, 4,
+                                  Fc, hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+      for (uint32_t f = 0; f < Fc; ++f) worst = std::max(worst, recs_n[c0 + f]);
+    }
+    // k_setup flags records past the cap; device frame records may flag a bad set
+    uint32_t ov = 0;
+    HIP_TRY(c, hipMemcpy(&ov, c->overflow.p, 4, hipMemcpyDeviceToHost));
+    if (ov) {
+      HIP_TRY(c, hipMemsetAsync(c->overflow.p, 0, 4, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+    }
+    if (ov & (kOvBadSet | kOvBadKpSet)) {
+      release_work(c);
+      return c->fail(CSG_ERR_INVALID, "size_work: device frame records named a transform set >= %u",
+                     (unsigned)c->set_valid.size());
+    }
+    if (worst <= cap) break;   // every frame's records were kept, so its bin total is exact
+    if (attempt == 3) {
+      release_work(c);
+      return c->fail(CSG_ERR_OVERFLOW, "size_work: a frame emitted %u records", worst);
+    }
+    cap = (uint32_t)std::min<uint64_t>(((uint64_t)worst + worst / 8 + 4096 + 3) & ~3ull, 0x7FFFFFF0ull);
+  }
+  release_work(c);
+  return CSG_OK;
+}
+
+static void fill_work_info(const csg_ctx* c, csg_work_info* out) {
+  memset(out, 0, sizeof(*out));
+  const uint32_t rec = c->rec_cap ? c->rec_cap : (c->cfg.records_per_frame ? c->cfg.records_per_frame : full_record_cap(c));
+  const uint32_t bin = c->bin_cap ? c->bin_cap
+                                  : (c->cfg.bins_per_frame ? c->cfg.bins_per_frame
+                                                           : (uint32_t)std::min<uint64_t>(3ull * rec + 16ull * c->n_tiles,
+                                                                                          0x7FFFFFFFull));
+  out->records_per_frame = rec;
+  out->bins_per_frame = bin;
+  out->frames_per_launch = c->chain_frames;
+  out->sized_frames = c->sized_frames;
+  out->max_records = c->sized_max_rec;
+  out->max_bins = c->sized_max_bin;
+  out->mean_records = c->sized_mean_rec;
+  out->mean_bins = c->sized_mean_bin;
+  out->work_bytes = work_bytes_for(c, c->chain_frames, rec, bin);
+}
+
+int csg_size_work(csg_ctx* c, const csg_frame* frames, uint32_t n, int32_t frames_on_device, float margin,
+                  csg_work_info* out) {
+  if (!c) return CSG_ERR_INVALID;
+  if (!frames || n == 0 || !(margin >= 0.0f) || margin > 64.0f)
+    return c->fail(CSG_ERR_INVALID, "size_work: need frames and a margin in [0, 64]");
+  if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "size_work: no scene uploaded");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  int rc = csg_synchronize(c);   // earlier batches done (their errors reported), flag clear
+  if (rc) return rc;
+  if (!frames_on_device)
+    for (uint32_t f = 0; f < n; ++f) {
+      const uint32_t set = frames[f].xform_set;
+      if (set >= c->set_valid.size() || !c->set_valid[set])
+        return c->fail(CSG_ERR_INVALID, "size_work: frame %u: transform set %u not uploaded", f, set);
+    }
+  rc = sync_scene_state(c);
+  if (rc) return rc;
+  std::vector<uint32_t> rn, bn;
+  rc = measure_work(c, frames, n, frames_on_device != 0, rn, bn);
+  if (rc) return rc;
+  uint32_t mr = 0, mb = 0;
+  double sr = 0.0, sb = 0.0;
+  for (uint32_t f = 0; f < n; ++f) {
+    mr = std::max(mr, rn[f]);
+    mb = std::max(mb, bn[f]);
+    sr += rn[f];
+    sb += bn[f];
+  }
+  const double k = 1.0 + (double)margin;
+  c->rec_cap = (uint32_t)std::min<uint64_t>((((uint64_t)std::ceil(mr * k) + 256 + 3) & ~3ull), 0x7FFFFFF0ull);
+  c->bin_cap = (uint32_t)std::min<uint64_t>((uint64_t)std::ceil(mb * k) + 1024, 0x7FFFFFFFull);
+  c->sized_frames = n;
+  c->sized_max_rec = mr;
+  c->sized_max_bin = mb;
+  c->sized_mean_rec = sr / n;
+  c->sized_mean_bin = sb / n;
+  release_work(c);   // the next batch allocates the work buffers at these caps
+  if (out) fill_work_info(c, out);
+  return CSG_OK;
+}
+
+int csg_get_work_info(csg_ctx* c, csg_work_info* out) {
+  if (!c || !out) return CSG_ERR_INVALID;
+  fill_work_info(c, out);
   return CSG_OK;
 }
 

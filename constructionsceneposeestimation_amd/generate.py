@@ -10,7 +10,8 @@ same files:
 
   rgb/rgb_%06d.png                 (:1672-1673)
   labels/label_%06d.json           (:2071-2072, schema :2056-2064 + keypoints_2d,
-                                    bbox_2d, pixel_count, occlusion_ratio)
+                                    bbox_2d, pixel_count; + occlusion_ratio with
+                                    --occlusion)
   labels/instance_mask_%06d.npy    (:2066-2069; real ids here, -1 background)
   depth/depth_%06d.csv             (:1687-1688)
   depth/depth_%06d.png             (:1690-1709, JET colour map made on the GPU)
@@ -101,11 +102,28 @@ def parse_outputs(spec: str) -> tuple:
     return out
 
 
+def render_outputs(outs: set, gpu_files: bool, host_depth: bool, occlusion: bool) -> list:
+    """The renderer outputs (renderer.OUTPUT_KINDS) a run with file outputs
+    ``outs`` asks for.  Label statistics and keypoints feed every label file;
+    the label coverage ("covered", k_raster<true>) only ``occlusion_ratio``,
+    which is not in the reference's label schema (GDP:2056-2064)."""
+    if gpu_files:
+        want = (["keypoints", "stats", "depth_stats"] + (["instance"] if "mask" in outs else [])
+                + (["depth"] if host_depth else []) + (["depth_range"] if "depth_png" in outs else [])
+                + (["normals"] if "normals" in outs else []))
+    else:
+        want = (["rgb", "instance", "keypoints", "stats"] + (["depth"] if host_depth else [])
+                + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
+                + (["normals"] if "normals" in outs else []))
+    return want + (["covered"] if occlusion else [])
+
+
 def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 0, batch: int = 30,
              device: int = 0, depth: bool = False, depth_csv: bool = False, pointcloud: bool = False,
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
              resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
-             writer_mode: str = "thread", renderers: int = 0, object_list: str = "visible") -> dict:
+             writer_mode: str = "thread", renderers: int = 0, object_list: str = "visible",
+             occlusion: bool = False) -> dict:
     """Render ``frames`` on one GPU and write them (``outputs``, default the
     reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
     add the depth .npy, the depth .npy + CSV, the point cloud, the normals).
@@ -116,7 +134,12 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     ``object_list``: "visible" lists the objects with visible pixels in each
     label file; "frustum" also those whose 3D box meets the view frustum
     (labels.label_record; the reference lists Replicator's bounding_box_3d
-    primPaths, whose inclusion rule is closed)."""
+    primPaths, whose inclusion rule is closed).
+    ``occlusion`` adds each object's ``occlusion_ratio`` (Replicator's
+    occlusionRatio) to the label files.  The reference never reads that field
+    and its label schema (GDP:2056-2064) has none, so it is off by default: it
+    needs the per-label unoccluded coverage, i.e. k_raster<true> (about +36%
+    raster time)."""
     if object_list not in OBJECT_LISTS:
         raise ValueError(f"object_list {object_list!r}: choose from {OBJECT_LISTS}")
     outs = set(REFERENCE_OUTPUTS if outputs is None else outputs)
@@ -142,14 +165,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     # the GPU (depth_stats) in thread mode, from the host depth otherwise
     host_depth = "depth_npy" in outs or (not gpu_files and bool(outs & {"depth_csv", "pointcloud"}))
     log = QualityLog(os.path.join(out_dir, "logs"))
-    if gpu_files:
-        want = (["keypoints", "stats", "covered", "depth_stats"] + (["instance"] if "mask" in outs else [])
-                + (["depth"] if host_depth else []) + (["depth_range"] if "depth_png" in outs else [])
-                + (["normals"] if "normals" in outs else []))
-    else:
-        want = (["rgb", "instance", "keypoints", "stats", "covered"] + (["depth"] if host_depth else [])
-                + (["depth_vis"] if "depth_png" in outs else []) + (["points"] if "pointcloud" in outs else [])
-                + (["normals"] if "normals" in outs else []))
+    want = render_outputs(outs, gpu_files, host_depth, occlusion)
     n_writers = writers or default_writers()
     # Renderer contexts on the device, each with its own stream and work
     # buffers, rendering alternate batches from their own threads: one batch's
@@ -172,6 +188,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     lw = LabelWriter(wl.kp_table, wl.intr.params(), scene_labels(wl.scene), wl.height, wl.width) if gpu_files else None
     pose_cache = {}
     pending = []
+
+    def cov_of(out, k):   # the frame's label coverage (occlusion_ratio), when rendered
+        return out["label_covered"][k] if "label_covered" in out else None
+
     t_render = t_slot_wait = t_prep = t_main_wait = t_labels = 0.0
     t0 = time.time()
     starts = list(range(0, len(frames), batch))
@@ -216,7 +236,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             outs_b = {k: v[:len(fb)] for k, v in arrays.items() if k not in ("files", "file_offsets")}
             out, offsets, need = r.render_files(fr, kinds, arrays["files"], want=want, out=outs_b)
             if offsets is None:   # the files did not fit: a larger buffer, no re-render
-                offsets = r.copy_files(pool.grow_files(slot, need + need // 4), len(fb) * nk)
+                offsets = r.copy_files(pool.grow_files(slot, need + need // 4, alloc=r.host_buffer,
+                                                       free=r.free_host_buffer), len(fb) * nk)
             arrays["file_offsets"] = offsets
         else:
             out = r.render(fr, want=want, out={k: v[:len(fb)] for k, v in arrays.items()})
@@ -256,13 +277,13 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 if lw is not None:
                     ep = lw.epoch(f // 10, pose_cache[f // 10])
                     lab = partial(lw.write, frame_id=f, camera_pose=cm.get_obj_pose_from_matrix(C), ep=ep,
-                                  inst_stats=out["inst_stats"][k], covered=out["label_covered"][k],
+                                  inst_stats=out["inst_stats"][k], covered=cov_of(out, k),
                                   kp_uv=out["keypoints_uv"][k], kp_vis=out["keypoints_vis"][k], listed=listed)
                     n_obj = lw.n_visible(ep, out["inst_stats"][k], listed)
                 else:
                     lab = label_record(f, cm.get_obj_pose_from_matrix(C), intr.params(), pose_cache[f // 10],
                                        out["inst_stats"][k], out["keypoints_uv"][k], out["keypoints_vis"][k],
-                                       wl.kp_table, wl.height, wl.width, covered=out["label_covered"][k],
+                                       wl.kp_table, wl.height, wl.width, covered=cov_of(out, k),
                                        listed=listed)
                     n_obj = lab["num_objects"]
                 log_args = dict(n_objects=n_obj, kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
@@ -276,7 +297,9 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 if kinds:   # GPU-encoded: file j = frame * nk + index of its kind
                     for o, kd in FILE_OF_OUTPUT:
                         if o in outs:
-                            files.append((file_path(out_dir, o, f), "encoded", (k * nk + kinds.index(kd),)))
+                            files.append((file_path(out_dir, o, f),
+                                          "encoded_pointcloud" if o == "pointcloud" else "encoded",
+                                          (k * nk + kinds.index(kd),)))
                 elif "rgb" in outs:
                     files.append((file_path(out_dir, "rgb", f), "png", ("rgb",)))
                 if "mask" in outs:
@@ -348,6 +371,9 @@ def main(argv=None):
                     help="renderer contexts rendering alternate batches (0: 2 with writer threads, else 1)")
     ap.add_argument("--object-list", default="visible", choices=OBJECT_LISTS,
                     help="objects in each label file: with visible pixels, or also every one in the view frustum")
+    ap.add_argument("--occlusion", action="store_true",
+                    help="add occlusion_ratio per object to the label files (not in the reference's schema; "
+                         "costs the unoccluded-coverage raster)")
     ap.add_argument("--no-resume", action="store_true")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
@@ -355,7 +381,7 @@ def main(argv=None):
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
                        a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
                        outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode, renderers=a.renderers,
-                       object_list=a.object_list)
+                       object_list=a.object_list, occlusion=a.occlusion)
     print(json.dumps(summary))
 
 

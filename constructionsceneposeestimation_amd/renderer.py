@@ -331,6 +331,27 @@ class Renderer:
         self._check(self.lib.csg_get_batch_stats(self.ctx, C.byref(st)), "get_batch_stats")
         return {n: getattr(st, n) for n, _ in _lib.BatchStats._fields_}
 
+    def size_work(self, frames, n: Optional[int] = None, on_device: bool = False,
+                  margin: float = 0.25) -> Dict[str, float]:
+        """Size the per-frame work buffers from a sizing pass over ``frames``
+        (csg_size_work): a FRAME_DTYPE array, or with ``on_device`` a device
+        pointer (int) to ``n`` frame records.  Returns :meth:`work_info`."""
+        info = _lib.WorkInfo()
+        if on_device:
+            self._check(self.lib.csg_size_work(self.ctx, int(frames), int(n), 1, float(margin), C.byref(info)),
+                        "size_work")
+        else:
+            fr = np.ascontiguousarray(frames, FRAME_DTYPE)
+            self._check(self.lib.csg_size_work(self.ctx, fr.ctypes.data, fr.shape[0], 0, float(margin),
+                                               C.byref(info)), "size_work")
+        return {k: getattr(info, k) for k, _ in _lib.WorkInfo._fields_}
+
+    def work_info(self) -> Dict[str, float]:
+        """Current work-buffer caps, the last sizing pass and the buffers' device bytes."""
+        info = _lib.WorkInfo()
+        self._check(self.lib.csg_get_work_info(self.ctx, C.byref(info)), "get_work_info")
+        return {k: getattr(info, k) for k, _ in _lib.WorkInfo._fields_}
+
     def timing_reset(self) -> None:
         self._check(self.lib.csg_timing_reset(self.ctx), "timing_reset")
 

@@ -61,6 +61,9 @@ def _write_bytes(path: str, data) -> None:
         os.close(fd)
 
 
+POINTCLOUD_HEADER = b"x y z r g b\n"   # the TXT's first line (np.savetxt header, GDP:766-770)
+
+
 def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, str, Tuple[str, ...]]],
                 label: dict, label_path: str) -> Optional[dict]:
     """Every file of frame ``k`` of a batch, then its label JSON (the resume
@@ -73,12 +76,20 @@ def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, st
     from . import writers as fileio
     from .labels import label_json_bytes
     for path, kind, keys in files:
-        if kind == "encoded":
+        if kind in ("encoded", "encoded_pointcloud"):
             off = arrays["file_offsets"]
             j = keys[0]
-            _atomic(path, _write_bytes, arrays["files"][int(off[j]):int(off[j + 1])])
+            data = arrays["files"][int(off[j]):int(off[j + 1])]
+            # a frame without a single point gets no point-cloud file, as in the
+            # reference (save_pointcloud_with_rgb returns on an empty cloud,
+            # GDP:723-725; the depth fallback saves only len(xyzrgb) > 0, :1755)
+            if kind == "encoded_pointcloud" and len(data) <= len(POINTCLOUD_HEADER):
+                continue
+            _atomic(path, _write_bytes, data)
             continue
         a = [arrays[x][k] for x in keys]
+        if kind == "pointcloud" and np.isnan(a[0]).all():   # no point: no file (GDP:723-725, :1755)
+            continue
         if kind == "png":
             _atomic(path, _write_png, *a)
         elif kind == "npy":
@@ -166,6 +177,8 @@ class WriterPool:
         assert self._local is not None, "pinned slots need writer threads"
         self.free = free
         self._grow_lock = threading.Lock()
+        self._files_free = {}          # slot -> free() of its current files buffer's renderer
+        self._retired = []             # (replaced files buffer, its free()), released in close()
         for slot in range(self.n_slots):
             buf = alloc(self.slot_bytes)
             d = {k: np.ndarray(shape, np.dtype(dt), buffer=buf, offset=off)
@@ -175,17 +188,24 @@ class WriterPool:
             self._local[slot] = d
         self.alloc = alloc
 
-    def grow_files(self, slot: int, nbytes: int) -> np.ndarray:
+    def grow_files(self, slot: int, nbytes: int, alloc=None, free=None) -> np.ndarray:
         """A larger ``files`` buffer for a slot (the batch's files did not
-        fit).  Called after :meth:`arrays` waited for the slot's tasks, so no
-        writer reads the old buffer: it is freed at once.  Render threads of
-        several renderers may grow at the same time; the allocator (one
-        renderer's context) is used under a lock."""
+        fit), from ``alloc`` / to be released by ``free``: the growing
+        renderer's own (Renderer.host_buffer / free_host_buffer), so a
+        renderer context is only touched by the thread that renders with it.
+        The replaced buffer is retired, not freed: it is released in
+        :meth:`close`, after every render thread has finished (hipHostFree
+        waits for the device, which would stall the other renderer's batch).
+        The lock orders concurrent grows of the renderers' threads."""
+        alloc = alloc or self.alloc
         with self._grow_lock:
             old = self._local[slot].get("files")
-            self._local[slot]["files"] = self.alloc(nbytes)
-            if old is not None and self.free is not None:
-                self.free(old)
+            self._local[slot]["files"] = alloc(nbytes)
+            if old is not None:
+                owner = self._files_free.get(slot, self.free)
+                if owner is not None:
+                    self._retired.append((old, owner))
+            self._files_free[slot] = free or self.free
         return self._local[slot]["files"]
 
     def arrays(self, slot: int) -> Dict[str, np.ndarray]:
@@ -224,6 +244,9 @@ class WriterPool:
             for f in fs:
                 f.result()
         self.pool.shutdown()
+        for arr, free in getattr(self, "_retired", []):
+            free(arr)
+        self._retired = []
         if self.shm is not None:
             try:
                 self.shm.close()

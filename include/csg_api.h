@@ -32,6 +32,9 @@
  *                               and of the point cloud           :1687-1709,
  *                                                                :714-775, :1716-1757
  *   csg_copy_files / csg_host_alloc / csg_host_free (pinned buffers for them)
+ *   csg_size_work / csg_get_work_info (per-frame work-buffer caps measured
+ *                               on a sample of frames; no reference counterpart:
+ *                               Kit sizes its own render buffers)
  *   csg_last_error / csg_destroy
  *
  * Threading: several contexts may share a device (each has its own stream
@@ -47,7 +50,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 8
+#define CSG_ABI_VERSION 9
 
 typedef enum {
   CSG_OK = 0,
@@ -252,6 +255,40 @@ int csg_copy_files(csg_ctx* ctx, uint8_t* dst, uint64_t cap, uint64_t* offsets);
 /* Page-locked host memory for csg_outputs.files and the other host outputs. */
 int csg_host_alloc(csg_ctx* ctx, uint64_t bytes, void** out);
 int csg_host_free(csg_ctx* ctx, void* p);
+
+/* Work-buffer sizing.  k_setup appends each frame's raster records into a
+ * fixed per-frame region of `records_per_frame` records and k_bin its tile
+ * lists into `bins_per_frame` entries; the buffers hold one launch chain
+ * (frames_per_launch frames).  With the config's caps 0 they are sized for
+ * every triangle of the scene (1.125 x triangles per frame, 3x that in bin
+ * entries), which no frame can overflow but which a typical view uses a
+ * fraction of (C3 1080p: ~1/5 of the records, ~1/9 of the bin entries).
+ *
+ * csg_size_work runs the sizing pass on `n_frames` frames (host records, or
+ * device records when frames_on_device = 1; any number, in chains of 64):
+ * k_clip, k_setup, k_count, k_colscan and k_scan only, no raster and no
+ * outputs; then sets the caps to the largest per-frame record and bin-entry
+ * counts among them times (1 + margin) (margin >= 0, e.g. 0.25), and frees
+ * the work buffers (the next batch allocates them at the new caps).  The
+ * counts are a pure function of the frame, so batches of the measured frames
+ * never overflow.  Other frames can: csg_render_batch then grows the caps and
+ * renders again; an asynchronous batch reports CSG_ERR_OVERFLOW at the next
+ * csg_synchronize.  Waits for the context's earlier batches first (and
+ * reports their errors). */
+typedef struct {
+  uint32_t records_per_frame;  /* current caps */
+  uint32_t bins_per_frame;
+  uint32_t frames_per_launch;  /* frames the work buffers hold (one launch chain) */
+  uint32_t sized_frames;       /* frames the last csg_size_work measured (0: none) */
+  uint32_t max_records;        /* largest per-frame counts it measured */
+  uint32_t max_bins;
+  double mean_records;         /* and their means */
+  double mean_bins;
+  uint64_t work_bytes;         /* device bytes of the work buffers at the current caps */
+} csg_work_info;
+int csg_size_work(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames, int32_t frames_on_device,
+                  float margin, csg_work_info* out);
+int csg_get_work_info(csg_ctx* ctx, csg_work_info* out);
 
 /* Stand-alone 3D->2D projection (host buffers): uv [n][2], vis [n] without a
  * depth test (1 = in front and inside the image, 0 otherwise). */

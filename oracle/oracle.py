@@ -199,7 +199,7 @@ class Oracle:
         vis = np.empty(pts.shape[0], np.int32)
         v = np.ascontiguousarray(view, np.float32).reshape(16)
         pr = np.ascontiguousarray(proj, np.float32).reshape(16)
-        d = np.ascontiguousarray(depth, np.float32)
+        d = None if depth is None else np.ascontiguousarray(depth, np.float32)   # None: no depth test
         lib().oracle_keypoints(C.byref(self.s), _ptr(v), _ptr(pr), _ptr(pts), pts.shape[0], _ptr(d),
                                _ptr(uv), _ptr(vis))
         return uv, vis

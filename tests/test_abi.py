@@ -49,7 +49,8 @@ def test_struct_layouts_match_c():
     from constructionsceneposeestimation_amd import _lib
     names = {"csg_config": _lib.Config, "csg_mesh": _lib.Mesh, "csg_material": _lib.Material,
              "csg_instance": _lib.Instance, "csg_light": _lib.Light, "csg_frame": _lib.Frame,
-             "csg_outputs": _lib.Outputs, "csg_batch_stats": _lib.BatchStats, "csg_timing": _lib.Timing}
+             "csg_outputs": _lib.Outputs, "csg_batch_stats": _lib.BatchStats, "csg_timing": _lib.Timing,
+             "csg_work_info": _lib.WorkInfo}
     prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"csg_api.h\"\nint main(){\n"
     for n in names:
         prog += f'printf("{n} %zu\\n", sizeof({n}));\n'

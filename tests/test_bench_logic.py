@@ -104,3 +104,30 @@ def test_elapsed_is_max_and_counts_sum_over_ranks_gloo(tmp_path):
 def test_default_frames_per_step_by_frame_size():
     assert bench.default_frames_per_step(1920, 1080) == bench.DEFAULT_FRAMES_PER_STEP
     assert bench.default_frames_per_step(3840, 2160) == bench.LARGE_FRAMES_PER_STEP < bench.DEFAULT_FRAMES_PER_STEP
+
+
+def test_shard_report_single_rank_and_gloo_pair(tmp_path):
+    import bench
+    r = bench.shard_report(list(range(20, 40)), 1)
+    assert r == {"ranks": 1, "timed_frames_per_rank": [20], "union": 20, "disjoint": True,
+                 "epochs_mod_world": [[0]]}
+    import torch.multiprocessing as mp
+    mp.spawn(_shard_worker, args=(_free_port(), str(tmp_path)), nprocs=2, join=True)
+    import json
+    rep = json.load(open(tmp_path / "rep.json"))
+    assert rep["disjoint"] and rep["union"] == 2 * 3 * 20 and rep["epochs_mod_world"] == [[0], [1]]
+
+
+def _shard_worker(rank, port, out_dir):
+    import json
+    import os
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    fids = bench.rank_frames(rank, 2, 4, 20)
+    rep = bench.shard_report(bench.timed_frames(fids, 1, 3, 20), 2)
+    if rank == 0:
+        json.dump(rep, open(os.path.join(out_dir, "rep.json"), "w"))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,0 +1,56 @@
+"""The bench's N>1 path as the driver's 8-GPU run starts it: two ranks under
+``torch.distributed.run`` (one process per rank, gloo for the barrier and the
+max-over-ranks; no data-path collective), sharing the box's one MI355X.
+
+The test process only starts a child (``subprocess.run``) and parses its JSON
+line: each rank renders its own epochs (e = r mod N), checks 4
+frames of its last timed step against the oracle, and the ranks' timed frame
+sets are disjoint.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(900)
+def test_bench_two_ranks_under_torchrun(tmp_path):
+    steps, warmup, F = 2, 1, 48
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", str(steps), "--warmup", str(warmup), "--frames-per-step", str(F),
+           "--verify-frames-multi", "4"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log = tmp_path / "bench2.err"
+    with open(log, "w") as err:
+        r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=err, text=True, timeout=840)
+    tail = log.read_text()[-4000:]
+    assert r.returncode == 0, f"bench at N=2 failed ({r.returncode}):\n{tail}"
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == steps and d["warmup"] == warmup
+    assert d["scaling"] == "weak" and d["value"] > 0
+    assert d["verified"]["frames"] == 8 and d["verified"]["bit_exact"] is True
+    sh = d["shards"]
+    assert sh["ranks"] == 2 and sh["disjoint"] is True
+    assert sh["timed_frames_per_rank"] == [steps * F, steps * F]
+    assert sh["union"] == 2 * steps * F
+    assert sh["epochs_mod_world"] == [[0], [1]]
+    # value = every rank's frames over the slowest rank's time
+    assert abs(d["value"] - 2 * steps * F / (d["ms_per_step"] * steps / 1e3)) <= 0.01 * d["value"]

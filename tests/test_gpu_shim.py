@@ -109,7 +109,13 @@ def test_generate_writes_reference_layout(tmp_path):
     assert (tmp_path / "depth" / "depth_000003.csv").read_text() == buf.getvalue()
     png = np.asarray(Image.open(tmp_path / "depth" / "depth_000003.png").convert("RGB"))
     assert np.array_equal(png, depth_vis(d3)[0])
-    for o in lab["objects"]:
+    # the default label files carry no occlusion_ratio (not in the reference's schema); --occlusion adds it
+    assert all("occlusion_ratio" not in o for o in lab["objects"])
+    occ = generate(str(tmp_path / "occ"), [11], "C3", seed=1, batch=5, width=160, height=96, occlusion=True)
+    assert occ["counters"]["successful_frames"] == 1
+    lab_occ = json.load(open(tmp_path / "occ" / "labels" / "label_000011.json"))
+    assert [o["inst_idx"] for o in lab_occ["objects"]] == [o["inst_idx"] for o in lab["objects"]]
+    for o in lab_occ["objects"]:
         assert 0.0 <= o["occlusion_ratio"] <= 1.0
     summ = json.load(open(tmp_path / "logs" / "generation_summary.json"))
     assert len(summ["frame_logs"]) == 12 and summ["statistics"]["successful_frames"] == 12

@@ -98,11 +98,11 @@ def _worker(rank, world, port, total, out_dir):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world,total", [(2, 40), (4, 80)])
+@pytest.mark.parametrize("world,total", [(2, 40), (4, 80), (8, 160)])
 def test_multi_rank_gloo_union_equals_single_process(tmp_path, world, total):
-    """world_size-2 and -4 runs over gloo: each rank renders only its epochs;
-    the union is bit-identical to a single-process render of every frame
-    (shards at n = 2/4 union to n = 1)."""
+    """world_size-2, -4 and -8 runs over gloo: each rank renders only its
+    epochs; the union is bit-identical to a single-process render of every
+    frame (shards at n = 2/4/8 union to n = 1)."""
     import pickle
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(world, _free_port(), total, str(tmp_path)), nprocs=world, join=True)

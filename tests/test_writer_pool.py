@@ -65,3 +65,53 @@ def test_writer_pool_process_matches_threads(tmp_path):
     assert names == sorted(os.listdir(tmp_path / "process")) and len(names) == 9 * 5
     for n in names:
         assert (tmp_path / "thread" / n).read_bytes() == (tmp_path / "process" / n).read_bytes(), n
+
+
+def test_grown_files_buffers_are_retired_until_close():
+    """grow_files allocates with the growing renderer's own allocator and
+    retires the replaced buffer (freed by its own renderer's free, in close(),
+    after the render threads are done), never frees it at once."""
+    from constructionsceneposeestimation_amd.writer_pool import WriterPool
+    events = []
+
+    def allocator(name):
+        def alloc(n):
+            a = np.zeros(n, np.uint8)
+            events.append(("alloc", name, n))
+            return a
+        return alloc
+
+    def freer(name):
+        return lambda a: events.append(("free", name, a.nbytes))
+
+    pool = WriterPool({"rgb": ((1, 4, 4, 3), np.uint8)}, workers=1, n_slots=2, mode="thread")
+    pool.use_pinned(allocator("r0"), files_bytes=100, free=freer("r0"))
+    pool.grow_files(0, 200, alloc=allocator("r1"), free=freer("r1"))
+    pool.grow_files(0, 300, alloc=allocator("r0"), free=freer("r0"))
+    assert pool.arrays(0)["files"].nbytes == 300
+    assert not [e for e in events if e[0] == "free"]          # nothing freed while rendering
+    pool.close()
+    assert [e for e in events if e[0] == "free"] == [("free", "r0", 100), ("free", "r1", 200)]
+
+
+def test_frames_without_points_get_no_pointcloud_file(tmp_path):
+    """The reference writes no point-cloud file for a frame without a single
+    point (save_pointcloud_with_rgb returns on an empty cloud, GDP:723-725;
+    the depth fallback saves only when len(xyzrgb) > 0, :1755): neither the
+    GPU-encoded file (header only) nor the host writer's."""
+    from constructionsceneposeestimation_amd.writer_pool import POINTCLOUD_HEADER, write_frame
+    hdr = np.frombuffer(POINTCLOUD_HEADER, np.uint8)
+    line = np.frombuffer(b"1.000000 2.000000 3.000000 4.000000 5.000000 6.000000\n", np.uint8)
+    files = np.concatenate([hdr, hdr, line])
+    offsets = np.array([0, hdr.size, files.size], np.uint64)
+    pts = np.full((1, 2, 2, 3), np.nan, np.float32)
+    rgb = np.zeros((1, 2, 2, 3), np.uint8)
+    arrays = {"files": files, "file_offsets": offsets, "points": pts, "rgb": rgb}
+    p = [str(tmp_path / n) for n in ("empty.txt", "one.txt", "host_empty.txt", "host_one.txt")]
+    write_frame(arrays, 0, [(p[0], "encoded_pointcloud", (0,)), (p[1], "encoded_pointcloud", (1,)),
+                            (p[2], "pointcloud", ("points", "rgb"))], {"frame_id": 0}, str(tmp_path / "l0.json"))
+    assert not os.path.exists(p[0]) and not os.path.exists(p[2])
+    assert open(p[1], "rb").read() == files[hdr.size:].tobytes()
+    pts[0, 1, 1] = (1.0, 2.0, 3.0)
+    write_frame(arrays, 0, [(p[3], "pointcloud", ("points", "rgb"))], {"frame_id": 0}, str(tmp_path / "l1.json"))
+    assert open(p[3], "rb").read() == POINTCLOUD_HEADER + b"1.000000 2.000000 3.000000 0.000000 0.000000 0.000000\n"

@@ -213,3 +213,39 @@ def test_in_frustum_box_cases():
         frames.append(M)
     got = labels.in_frustum(SimpleNamespace(objects=objs), frames, V, P, W, H, intr.near, intr.far)
     assert got.tolist() == [True, False, False, False, True]
+
+
+def test_reference_mode_labels_have_no_occlusion_ratio(tmp_path):
+    """The generator's default (``--outputs reference``) renders no label
+    coverage, so its label files carry no occlusion_ratio (absent from the
+    reference's schema, GDP:2056-2064); the native writer's file still matches
+    label_record byte for byte.  ``--occlusion`` asks for the coverage."""
+    from constructionsceneposeestimation_amd import camera_math as cm
+    from constructionsceneposeestimation_amd import labels
+    from constructionsceneposeestimation_amd.generate import REFERENCE_OUTPUTS, main, render_outputs
+    from constructionsceneposeestimation_amd.renderer import scene_labels
+    from constructionsceneposeestimation_amd.workload import Workload
+    from constructionsceneposeestimation_amd.writers import LabelWriter
+    for gpu_files in (True, False):
+        for host_depth in (True, False):
+            assert "covered" not in render_outputs(set(REFERENCE_OUTPUTS), gpu_files, host_depth, False)
+            assert "covered" in render_outputs(set(REFERENCE_OUTPUTS), gpu_files, host_depth, True)
+            assert {"keypoints", "stats"} <= set(render_outputs(set(REFERENCE_OUTPUTS), gpu_files, host_depth, False))
+    wl = Workload("C3", seed=0)
+    nl, K = scene_labels(wl.scene), wl.n_keypoints()
+    lw = LabelWriter(wl.kp_table, wl.intr.params(), nl, wl.height, wl.width)
+    rng = np.random.default_rng(3)
+    for f in (4, 77):
+        poses = labels.object_poses(wl.scene, wl.epoch(f // 10).object_frames)
+        stats = rng.integers(1, 1000, (nl, 5)).astype(np.uint32)
+        uv = (rng.standard_normal((K, 2)) * 800).astype(np.float32)
+        vis = rng.integers(0, 3, K).astype(np.int32)
+        pose = cm.get_obj_pose_from_matrix(wl.camera(f)[2])
+        lab = labels.label_record(f, pose, wl.intr.params(), poses, stats, uv, vis, wl.kp_table, wl.height, wl.width)
+        assert lab["objects"] and all("occlusion_ratio" not in o for o in lab["objects"])
+        path = str(tmp_path / f"label_{f}.json")
+        lw.write(path, f, pose, lw.epoch(f // 10, poses), stats, None, uv, vis)
+        data = open(path, "rb").read()
+        assert data == labels.label_json_bytes(lab) and b"occlusion_ratio" not in data
+    with pytest.raises(SystemExit):   # the CLI knows the switch (argparse exits on --help)
+        main(["--out", str(tmp_path), "--occlusion", "--help"])

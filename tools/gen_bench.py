@@ -103,21 +103,33 @@ def main():
     ap.add_argument("--outputs", default="reference")
     ap.add_argument("--writer-mode", default="thread", choices=("thread", "process"))
     ap.add_argument("--renderers", type=int, default=0)
+    ap.add_argument("--occlusion", action="store_true", help="labels with occlusion_ratio (k_raster<true>)")
+    ap.add_argument("--skip-extras", action="store_true", help="only the generator run (no encode costs, disk probes)")
     ap.add_argument("--dir", default=None, help="file system to write to (default $TMPDIR; /dev/shm: RAM)")
     a = ap.parse_args()
     outputs = parse_outputs(a.outputs)
     out = tempfile.mkdtemp(prefix="csg_gen_", dir=a.dir)
     try:
         generate(out, list(range(a.batch)), a.workload, seed=9, batch=a.batch, writers=a.writers,
-                 outputs=outputs, writer_mode=a.writer_mode, renderers=a.renderers)   # warm-up
+                 outputs=outputs, writer_mode=a.writer_mode, renderers=a.renderers,
+                 occlusion=a.occlusion)   # warm-up
         shutil.rmtree(out)
         t0 = time.perf_counter()
         s = generate(out, list(range(a.frames)), a.workload, seed=0, batch=a.batch, writers=a.writers,
-                     outputs=outputs, writer_mode=a.writer_mode, renderers=a.renderers)
+                     outputs=outputs, writer_mode=a.writer_mode, renderers=a.renderers, occlusion=a.occlusion)
         dt = time.perf_counter() - t0
         size = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(out) for f in fs)
         shutil.rmtree(out)
         os.makedirs(out)
+        if a.skip_extras:
+            print(json.dumps({"frames": a.frames, "seconds": round(dt, 3), "frames_per_s": s["throughput"]["frames_per_s"],
+                              "frames_per_s_incl_setup": round(a.frames / dt, 1), "occlusion": a.occlusion,
+                              "render_thread": s["throughput"]["render_thread"], "main_thread": s["throughput"]["main_thread"],
+                              "wall_s": s["throughput"]["wall_s"], "writers": a.writers,
+                              "renderers": s["throughput"]["renderers"], "dir": os.path.dirname(out),
+                              "bytes_per_frame": round(size / a.frames), "workload": a.workload,
+                              "outputs": list(outputs) + ["label.json"], "successful": s["counters"]["successful_frames"]}))
+            return
         ms, sizes = encode_costs(a.workload, out, outputs)
         enc = sum(ms.values())
         gbs = disk_write(out)
@@ -130,7 +142,7 @@ def main():
             gbs_pinned = disk_write(out, src=pinned)
         print(json.dumps({
             "frames": a.frames, "seconds": round(dt, 3), "frames_per_s": s["throughput"]["frames_per_s"],
-            "frames_per_s_incl_setup": round(a.frames / dt, 1),
+            "frames_per_s_incl_setup": round(a.frames / dt, 1), "occlusion": a.occlusion,
             "render_s": s["throughput"]["render_s"], "render_thread": s["throughput"]["render_thread"],
             "main_thread": s["throughput"]["main_thread"], "wall_s": s["throughput"]["wall_s"], "writers": a.writers, "writer_mode": a.writer_mode,
             "renderers": s["throughput"]["renderers"], "dir": os.path.dirname(out), "bytes_written": size,
