@@ -48,17 +48,16 @@ sys.path.insert(0, ROOT)
 METRIC = "annotated frames/sec (RGB+seg+2D kpts) at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 RECORD_BYTES = 80 + 4  # k_setup writes one 80-B raster record + its 4-B tile rectangle per record
-# 960 frames per step = one launch chain: the kernels' ramp-down and the short
-# kernels' fixed cost are paid once per launch (C3, frames/s: 240 -> 22.09k,
-# 480 -> 22.20k, 960 -> 22.51k, 1,600 -> 22.60k, 1,920 -> 22.73k;
-# profiles/r03/ab/frames_per_step.txt).  960 keeps a rank's work buffers near
-# 100 GB (the library sizes them for every triangle of every frame), so two
-# ranks still share one MI355X in a rehearsal
-DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 20, 3, 960
-# Larger frames (C5 at 3840x2160 with depth, normals and points: ~200 MB of
-# outputs per frame) keep the round-2 step of 240 frames, so a rank stays
-# within one GPU's 288 GB.
-LARGE_FRAME_PIXELS, LARGE_FRAMES_PER_STEP = 1920 * 1080, 240
+# 2,880 frames per step = one launch chain: the kernels' ramp-down and the
+# short kernels' fixed cost are paid once per launch (C3 frames/s with the work
+# buffers sized by csg_size_work: 960 -> 22.62k, 1,920 -> 22.80k, 2,880 ->
+# 22.90k, 3,840 -> 22.92k; profiles/r04/ab/frames_per_step.txt).  At 2,880 a
+# rank holds ~120 GB of work buffers and ~42 GB of outputs on its 288-GB GPU.
+DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 10, 2, 2880
+# Larger frames (C5 at 3840x2160 with depth, normals and points: ~240 MB of
+# outputs per frame) take 480 frames per step (240 -> 6.30k, 480 -> 6.34k
+# frames/s): ~115 GB of outputs and ~28 GB of work per rank.
+LARGE_FRAME_PIXELS, LARGE_FRAMES_PER_STEP = 1920 * 1080, 480
 
 
 def default_frames_per_step(width: int, height: int) -> int:

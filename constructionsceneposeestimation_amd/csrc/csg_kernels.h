@@ -54,15 +54,19 @@ static_assert(sizeof(Chunk) == 48, "Chunk layout");
 // screen-space planes of its ORIGINAL triangle (spec §3.5-6): 1/W and, for
 // alpha-tested materials, u/W and v/W.  Field groups of 16 B as k_setup
 // writes and k_raster stages them: 0 x0 x1 x2 y0 | 1 y1 y2 p0 p1 |
-// 2 uid atex D0 D1 | 3 D2 U0 U1 U2 | 4 V0 V1 V2 atex_wh.
+// 2 uid atex D0 D1 | 3 U0 V0 U1 V1 | 4 U2 V2 D2 atex_wh.  The u and v planes
+// are interleaved so that (U_k, V_k) is an aligned register pair after the
+// 16-B LDS read: k_raster evaluates both planes with packed FP32
+// (v_pk_mul_f32 / v_pk_add_f32), each component in the spec's order.
 struct __attribute__((aligned(16))) Rec {
   int32_t x[3], y[3];          // 24: 24.8 fixed point, positive orientation
   uint16_t px0, py0, px1, py1; // 8 : inclusive pixel bbox, clamped to the frame
   uint32_t uid;                // 4
   uint32_t atex;               // 4 : alpha test (kNoAlpha: none): texel offset / 16 | threshold << 24
                                //     (keep iff alpha > threshold; texture offsets are 16-texel aligned)
-  float D[3];                  // 12: 1/W = (D0*x + D1*y) + D2 at pixel centre (x, y)
-  float U[3], V[3];            // 24: u/W, v/W planes (alpha-tested materials; zeros otherwise)
+  float D0, D1;                // 8 : 1/W = (D0*x + D1*y) + D2 at pixel centre (x, y)
+  float UV[3][2];              // 24: (u/W, v/W) plane coefficient pairs (alpha-tested materials; zeros otherwise)
+  float D2;                    // 4
   uint32_t atex_wh;            // 4 : alpha texture width | height << 16
 };
 static_assert(sizeof(Rec) == 80, "Rec layout");

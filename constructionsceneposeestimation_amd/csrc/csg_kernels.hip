@@ -65,6 +65,35 @@ __device__ __forceinline__ void mat4_mul(const float* a, const float* b, float* 
                      a[i * 4 + 3] * b[3 * 4 + j];
 }
 
+// 1.0f / x, bit-identical to the IEEE division for |x| in [2^-126, 2^126]:
+// the hardware reciprocal (~1 ulp) plus one Newton step with an exact FMA
+// residual, 3 VALU instead of the division's 11 (v_div_scale x2, v_rcp, 6 FMAs,
+// v_div_fmas, v_div_fixup).  Checked exhaustively on the MI355X over every
+// normal float of both signs (tools/rcp_check.hip, profiles/r04/rcp_check.json):
+// the only differences are the 2 x (2^24 - 1) x with |x| > 2^126, whose
+// reciprocal is subnormal.  Callers pass values inside the range (inverse
+// depths in [1/far, 1/near]); the `_any` form checks it and divides outside
+// (clip w, determinants).  CSG_FAST_RCP=0 builds the division everywhere (A/B).
+#ifndef CSG_FAST_RCP
+#define CSG_FAST_RCP 1
+#endif
+__device__ __forceinline__ float rcp_ieee(float x) {
+#if CSG_FAST_RCP
+  const float r0 = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, r0, 1.0f);
+  return __builtin_fmaf(e, r0, r0);
+#else
+  return 1.0f / x;
+#endif
+}
+__device__ __forceinline__ float rcp_ieee_any(float x) {
+  float r = rcp_ieee(x);
+  if (!(fabsf(x) >= 0x1p-126f && fabsf(x) <= 0x1p126f)) r = 1.0f / x;   // zero, denormal, huge, inf, NaN
+  return r;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));   // packed FP32 pair (v_pk_*_f32)
+
 struct Cv3 { float x, y, w; };
 
 struct Hom {
@@ -84,7 +113,7 @@ __device__ __forceinline__ void hom_setup(const Cv3* v, Hom& h) {
   }
   const float det = (v[0].x * h.A[0] + v[0].y * h.B[0]) + v[0].w * h.C[0];
   h.ok = det != 0.0f;
-  h.invdet = h.ok ? 1.0f / det : 0.0f;
+  h.invdet = h.ok ? rcp_ieee_any(det) : 0.0f;
 }
 
 // Screen-space planes of the original triangle (spec §3.5-6), from its
@@ -383,18 +412,24 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
       nwm += __any(nw >= k) ? 1 : 0;
       nhm += __any(nh >= k) ? 1 : 0;
     }
+    // E(i, j) = e0 + sx*i + sy*j stepped by additions (the same integers; a
+    // constant multiple such as sx*3 otherwise became a quarter-rate v_mul_lo_u32)
+    int32_t er[3] = {e0[0], e0[1], e0[2]};
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       if (j > nhm) break;
+      int32_t ec[3] = {er[0], er[1], er[2]};
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         if (i > nwm) break;
-        bool in = i <= nw && j <= nh;
-#pragma unroll
-        for (int e = 0; e < 3; ++e) in &= e0[e] + sx[e] * i + sy[e] * j >= 0;
+        const bool in = i <= nw && j <= nh && (ec[0] | ec[1] | ec[2]) >= 0;
         cols |= in ? 1u << i : 0u;
         rows |= in ? 1u << j : 0u;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) ec[e] += sx[e];
       }
+#pragma unroll
+      for (int e = 0; e < 3; ++e) er[e] += sy[e];
     }
     if (!cols) return false;
     px1 = px0 + 31 - __clz(cols);
@@ -544,7 +579,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
       auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
         // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c)
         float su[3], sv[3];
-        const float ra = 1.0f / a.w, rb = 1.0f / bb.w, rc = 1.0f / cc.w;
+        const float ra = rcp_ieee_any(a.w), rb = rcp_ieee_any(bb.w), rc = rcp_ieee_any(cc.w);
         su[0] = a.x * ra; sv[0] = a.y * ra;
         su[1] = bb.x * rb; sv[1] = bb.y * rb;
         su[2] = cc.x * rc; sv[2] = cc.y * rc;
@@ -580,8 +615,8 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
             uv_planes(h.A, h.B, h.C, h.invdet, uv, U, V);
           }
           c2 = make_uint4(uid, atex, __float_as_uint(D[0]), __float_as_uint(D[1]));
-          c3 = make_uint4(__float_as_uint(D[2]), __float_as_uint(U[0]), __float_as_uint(U[1]), __float_as_uint(U[2]));
-          c4 = make_uint4(__float_as_uint(V[0]), __float_as_uint(V[1]), __float_as_uint(V[2]), atex_wh);
+          c3 = make_uint4(__float_as_uint(U[0]), __float_as_uint(V[0]), __float_as_uint(U[1]), __float_as_uint(V[1]));
+          c4 = make_uint4(__float_as_uint(U[2]), __float_as_uint(V[2]), __float_as_uint(D[2]), atex_wh);
         }
       }
     }
@@ -1012,16 +1047,17 @@ __device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
 template <bool kCov, int NS>
 __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>& I, int k, int lx, int ly) {
   const float fx = (float)(c.ox + lx) + 0.5f, fy = (float)(c.oy + ly) + 0.5f;
-  const uint4 g2 = I.q[2][k], g3 = I.q[3][k];
-  const float invw = plane_at(f_(g2.z), f_(g2.w), f_(g3.x), fx, fy);
+  const uint4 g2 = I.q[2][k], g4 = I.q[4][k];
+  const float invw = plane_at(f_(g2.z), f_(g2.w), f_(g4.z), fx, fy);
   if (!(invw >= c.inv_far && invw <= c.inv_near)) return;
-  // alpha test at the pixel centre: u = U(x, y) * (1 / (1/W)), v likewise
+  // alpha test at the pixel centre: u = U(x, y) * (1 / (1/W)), v likewise;
+  // both planes at once in packed FP32, per component ((U0*x + U1*y) + U2) * r
   auto alpha_ok = [&]() {
-    const uint4 g4 = I.q[4][k];
-    const float r = 1.0f / invw;
-    const float u = plane_at(f_(g3.y), f_(g3.z), f_(g3.w), fx, fy) * r;
-    const float v = plane_at(f_(g4.x), f_(g4.y), f_(g4.z), fx, fy) * r;
-    return alpha_pass(c.aquad, c.acls, (g2.y & 0xFFFFFFu) * kTexAlign, g4.w, (int)(g2.y >> 24), u, v);
+    const uint4 g3 = I.q[3][k];
+    const float r = rcp_ieee(invw);   // invw in [1/far, 1/near]
+    const f32x2 p0 = {f_(g3.x), f_(g3.y)}, p1 = {f_(g3.z), f_(g3.w)}, p2 = {f_(g4.x), f_(g4.y)};
+    const f32x2 uv = ((p0 * fx + p1 * fy) + p2) * r;
+    return alpha_pass(c.aquad, c.acls, (g2.y & 0xFFFFFFu) * kTexAlign, g4.w, (int)(g2.y >> 24), uv.x, uv.y);
   };
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
   unsigned long long* z = &c.zb[ly * kTile + lx];
@@ -1376,7 +1412,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
   const bool textured = e.tex >= 0 && !(DBG(s.dbg) & 4096u);   // 4096: ablation only, no texture fetch
   const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
   float r = INFINITY;
-  if (need_depth || textured) r = 1.0f / plane_at(e.P[0], e.P[1], e.P[2], fx, fy);
+  if (need_depth || textured) r = rcp_ieee(plane_at(e.P[0], e.P[1], e.P[2], fx, fy));   // the winner's invW
   depth_out = need_depth ? r : INFINITY;
   id_out = e.label;
   int base[3] = {(int)(e.base & 255u), (int)((e.base >> 8) & 255u), (int)((e.base >> 16) & 255u)};
@@ -1609,7 +1645,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       const int px = (int)(pp & 0xFFFFu) - ox, py = (int)(pp >> 16) - oy;
       if (pp == 0xFFFFFFFFu || px < 0 || px >= kTile || py < 0 || py >= kTile) continue;
       const unsigned long long key = zb[py * kTile + px];
-      const float d = key == kEmptyKey ? INFINITY : 1.0f / __uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32));
+      const float d = key == kEmptyKey ? INFINITY : rcp_ieee(__uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32)));
       b.kp_vis[o] = (b.kp_w[o] <= d) ? 2 : 1;
     }
   }
@@ -1688,8 +1724,8 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
 #pragma unroll
       for (int w = 1; w < kBlock / 64; ++w) { kmn = min(kmn, drw[0][w]); kmx = max(kmx, drw[1][w]); }
       if (kmn <= kmx) {   // some pixel has a surface: depths 1/invW, valid (finite, > 0) by the depth range test
-        const float dmin = 1.0f / __uint_as_float(0xFFFFFFFFu - kmn);
-        const float dmax = 1.0f / __uint_as_float(0xFFFFFFFFu - kmx);
+        const float dmin = rcp_ieee(__uint_as_float(0xFFFFFFFFu - kmn));
+        const float dmax = rcp_ieee(__uint_as_float(0xFFFFFFFFu - kmx));
         // skip the atomic when the frame's range already holds it (most tiles)
         if (__float_as_uint(dmin) < b.drange[f]) atomicMin(&b.drange[f], __float_as_uint(dmin));
         if (__float_as_uint(dmax) > b.drange[b.drange_F + f]) atomicMax(&b.drange[b.drange_F + f], __float_as_uint(dmax));

@@ -2,7 +2,8 @@
 
 * C3 exactly as bench.py times it: 1920x1080, world2 + crane/dumper/human
   proxies, 2D keypoints, seed 0, frames drawn from the bench's timed steps
-  (warm-up 3, steps 20, bench.DEFAULT_FRAMES_PER_STEP frames per step) -- bit-exact.
+  (bench.DEFAULT_WARMUP warm-up steps, bench.DEFAULT_STEPS timed steps of
+  bench.DEFAULT_FRAMES_PER_STEP frames) -- bit-exact.
 * C2: 32 frames sampled across the scheduled 1,000-pose sequence of world2
   static (BASELINE configs[1]: 1920x1080, randomised camera poses) --
   bit-exact.
@@ -41,8 +42,12 @@ def test_c3_1080p_on_the_bench_timed_frames():
     from oracle.oracle import Oracle
     F, W, K = bench.DEFAULT_FRAMES_PER_STEP, bench.DEFAULT_WARMUP, bench.DEFAULT_STEPS
     timed = bench.timed_frames(bench.rank_frames(0, 1, W + K, F), W, K, F)
-    frames = [timed[0], timed[F + 17], timed[5 * F + 123], timed[11 * F + 200], timed[17 * F + 9], timed[-1]]
-    assert min(frames) >= 1200 - 480 and len(set(f // 10 for f in frames)) == len(frames)
+    n = len(timed)
+    assert n == K * F
+    # the first and last timed frames and four spread between, in different epochs
+    frames = [timed[0], timed[n // 7 + 17], timed[2 * n // 5 + 123], timed[3 * n // 5 + 200], timed[6 * n // 7 + 9],
+              timed[-1]]
+    assert min(frames) >= W * F and len(set(f // 10 for f in frames)) == len(frames)
     wl = Workload("C3", seed=0)
     assert (wl.width, wl.height) == (1920, 1080)
     V, P, gpu = _render_frames(wl, frames, ("rgb", "instance", "depth", "keypoints", "stats"))

@@ -16,14 +16,33 @@ N_SIMD = 256 * 4    # MI355X: 256 CUs x 4 SIMDs
 N_XCD = 8
 
 
+def _grid(row):
+    if "Grid_Size" in row:
+        return int(row["Grid_Size"] or 0)
+    g = 1
+    for a in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"):
+        g *= int(row.get(a) or 1)
+    return g
+
+
 def load(d):
-    per = defaultdict(lambda: defaultdict(list))
+    """Per kernel and counter, the values of the dispatches with the kernel's
+    largest grid: bench.py's sizing pass (csg_size_work) launches the setup
+    and binning kernels on 64-frame chains before the timed steps, and those
+    dispatches are not the bench's launches."""
+    rows = defaultdict(list)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
             name = row.get("Kernel_Name", "")
             short = (name.replace("(anonymous namespace)::", "").split("(")[0].replace("csg::", "")
                      .replace("void ", "").split("<")[0].strip())
-            per[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            rows[short].append((_grid(row), row["Counter_Name"], float(row["Counter_Value"])))
+    per = defaultdict(lambda: defaultdict(list))
+    for short, rs in rows.items():
+        gmax = max(g for g, _, _ in rs)
+        for g, c, v in rs:
+            if g == gmax:
+                per[short][c].append(v)
     return per
 
 
