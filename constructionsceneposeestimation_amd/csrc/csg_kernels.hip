@@ -52,6 +52,8 @@ constexpr float kGuardPx = 1048576.0f;
 // ---------------------------------------------------------------------------
 // shared arithmetic (mirrors csg_oracle.c line by line)
 // ---------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));   // packed FP32 pair (v_pk_*_f32)
+
 __device__ __forceinline__ float dot4(const float* r, float x, float y, float z) {
   return ((r[0] * x + r[1] * y) + r[2] * z) + r[3];
 }
@@ -91,8 +93,6 @@ __device__ __forceinline__ float rcp_ieee_any(float x) {
   if (!(fabsf(x) >= 0x1p-126f && fabsf(x) <= 0x1p126f)) r = 1.0f / x;   // zero, denormal, huge, inf, NaN
   return r;
 }
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));   // packed FP32 pair (v_pk_*_f32)
 
 struct Cv3 { float x, y, w; };
 
@@ -160,9 +160,15 @@ __device__ __forceinline__ int wrap_index(float fu, int n) {
   return (int)r;
 }
 
+// Texel coordinates (u * tw - 0.5, (1 - v) * th - 0.5) as one packed multiply and add
+__device__ __forceinline__ f32x2 texel_coords(float u, float v, int tw, int th) {
+  const f32x2 a = {u, 1.0f - v}, n = {(float)tw, (float)th};
+  return a * n - 0.5f;
+}
+
 __device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {   // tw, th <= 16384
-  float tu = u * (float)tw - 0.5f;
-  float tv = (1.0f - v) * (float)th - 0.5f;
+  const f32x2 t2 = texel_coords(u, v, tw, th);
+  float tu = t2.x, tv = t2.y;
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
@@ -220,8 +226,8 @@ __device__ __forceinline__ void tex_sample(const SceneDev& s, int tid, float u, 
 __device__ __forceinline__ bool alpha_pass(const uint32_t* aquad, const uint32_t* acls, uint32_t offset, uint32_t wh,
                                            int thr, float u, float v) {
   const int tw = (int)(wh & 0xFFFFu), th = (int)(wh >> 16);
-  float tu = u * (float)tw - 0.5f;
-  float tv = (1.0f - v) * (float)th - 0.5f;
+  const f32x2 t2 = texel_coords(u, v, tw, th);
+  float tu = t2.x, tv = t2.y;
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
@@ -1400,8 +1406,10 @@ __device__ __forceinline__ void shade_setup(const SceneDev& s, const BatchDev& b
   float D[3], U[3], V[3];
   depth_plane(P, P + 3, P + 6, P[9], D);
   uv_planes(P, P + 3, P + 6, P[9], P + 10, U, V);
+  // D in P[0..2]; the u and v planes as aligned (U_k, V_k) pairs in P[4..9]
+  // for shade_pixel's packed evaluation
 #pragma unroll
-  for (int z = 0; z < 3; ++z) { e.P[z] = D[z]; e.P[3 + z] = U[z]; e.P[6 + z] = V[z]; }
+  for (int z = 0; z < 3; ++z) { e.P[z] = D[z]; e.P[4 + 2 * z] = U[z]; e.P[5 + 2 * z] = V[z]; }
 }
 
 // Depth, instance id and RGB of pixel (px, py) covered by entry e.
@@ -1417,11 +1425,11 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
   id_out = e.label;
   int base[3] = {(int)(e.base & 255u), (int)((e.base >> 8) & 255u), (int)((e.base >> 16) & 255u)};
   int alb[3];
-  if (textured) {
-    const float u = plane_at(e.P[3], e.P[4], e.P[5], fx, fy) * r;
-    const float v = plane_at(e.P[6], e.P[7], e.P[8], fx, fy) * r;
+  if (textured) {   // u, v in packed FP32, per component ((U0*x + U1*y) + U2) * r
+    const f32x2 p0 = {e.P[4], e.P[5]}, p1 = {e.P[6], e.P[7]}, p2 = {e.P[8], e.P[9]};
+    const f32x2 uv = ((p0 * fx + p1 * fy) + p2) * r;
     int c[4];
-    tex_sample(s, e.tex, u, v, c);
+    tex_sample(s, e.tex, uv.x, uv.y, c);
 #pragma unroll
     for (int z = 0; z < 3; ++z) alb[z] = div255(__umul24((uint32_t)c[z], (uint32_t)base[z]) + 127u);
   } else {
@@ -1648,6 +1656,13 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
       const float d = key == kEmptyKey ? INFINITY : rcp_ieee(__uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32)));
       b.kp_vis[o] = (b.kp_w[o] <= d) ? 2 : 1;
     }
+    // The resolve below overwrites background z-buffer words (with the sky
+    // word) before its first barrier: every keypoint must have read its key
+    // first.  (Without this barrier a keypoint over the sky could read the sky
+    // word, whose depth field is 0: harmless with the IEEE 1/0 = +inf, a NaN
+    // with the Newton reciprocal, found by the bench's own verification.)
+    // The branch is uniform over the block (frame and tile).
+    __syncthreads();
   }
   // Label statistics (pixel count + tight box per label) only when the caller
   // asked for them (csg_outputs.inst_stats): otherwise no LDS table, no runs.

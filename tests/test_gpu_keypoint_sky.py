@@ -1,0 +1,68 @@
+"""Keypoints over sky pixels of tiles that hold geometry, many times over.
+
+k_raster's keypoint depth test reads the tile's z-buffer; the resolve then
+overwrites background words with the sky word.  A keypoint over a sky pixel
+must read the empty key (depth +inf: visible, 2) however the block's threads
+interleave -- round 4 found a missing barrier there through the bench's own
+verification (a keypoint could read the sky word, whose reciprocal is NaN with
+the Newton reciprocal).  Here: 400+ such keypoints at 100 m along sky-pixel rays
+of mixed tiles, 24 frames per batch, 4 batches; every one must be visible (2),
+and the result must equal the oracle's.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_keypoints_over_sky_in_mixed_tiles_are_visible_every_time():
+    from constructionsceneposeestimation_amd.packing import pack_scene
+    from constructionsceneposeestimation_amd.renderer import Renderer, make_frames
+    from constructionsceneposeestimation_amd.workload import Workload
+    from oracle.oracle import Oracle
+    wl = Workload("C3", seed=0, width=640, height=360)
+    W, H = wl.width, wl.height
+    o = Oracle(pack_scene(wl.scene), W, H)
+    frame = next(f for f in range(0, 4000, 37) if _sky_share(o, wl, f) > 0.2)
+    st = wl.epoch(frame // 10)
+    V, P = wl.frame_params([frame])
+    o.set_instance_models(st.models.reshape(-1, 16))
+    depth = o.render(V[0], P[0])["depth"]
+    sky = ~np.isfinite(depth)
+    # sky pixels of 32x32 tiles that also hold geometry
+    mixed = np.zeros_like(sky)
+    for ty in range(0, H, 32):
+        for tx in range(0, W, 32):
+            t = sky[ty:ty + 32, tx:tx + 32]
+            if t.any() and not t.all():
+                mixed[ty:ty + 32, tx:tx + 32] = t
+    ys, xs = np.nonzero(mixed)
+    assert len(ys) > 400
+    pick = np.random.default_rng(0).choice(len(ys), 400, replace=False)
+    p = wl.intr.params()
+    fx = p["width"] * p["focal_length"] / p["horizontal_aperture"]
+    fy = p["height"] * p["focal_length"] / p["vertical_aperture"]
+    C = wl.camera(frame)[2]
+    u, v, d = xs[pick] + 0.5, ys[pick] + 0.5, 100.0
+    cam = np.stack([(u - W / 2.0) * d / fx, -(v - H / 2.0) * d / fy, np.full(len(u), -d)], 1)
+    kp = (cam @ C[:3, :3].T + C[:3, 3]).astype(np.float32)
+    F = 24
+    frames = make_frames(np.repeat(V, F, 0), np.repeat(P, F, 0), [0] * F, [frame] * F)
+    ref_uv, ref_vis = o.keypoints(V[0], P[0], kp, depth)
+    inview = ref_vis > 0
+    assert inview.sum() > 350 and (ref_vis[inview] == 2).all()
+    with Renderer(wl.scene, W, H, max_frames=F) as r:
+        r.set_instance_transforms(0, st.models)
+        r.set_keypoints(0, kp)
+        for _ in range(4):
+            out = r.render(frames, want=("instance", "keypoints"))
+            assert np.array_equal(out["keypoints_vis"], np.broadcast_to(ref_vis, out["keypoints_vis"].shape))
+            assert np.array_equal(out["keypoints_uv"].view(np.uint32),
+                                  np.broadcast_to(ref_uv.view(np.uint32), out["keypoints_uv"].shape))
+
+
+def _sky_share(o, wl, f):
+    st = wl.epoch(f // 10)
+    V, P = wl.frame_params([f])
+    o.set_instance_models(st.models.reshape(-1, 16))
+    return float((~np.isfinite(o.render(V[0], P[0])["depth"])).mean())
