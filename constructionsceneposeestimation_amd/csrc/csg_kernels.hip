@@ -73,9 +73,11 @@ __device__ __forceinline__ void mat4_mul(const float* a, const float* b, float* 
 // v_div_fmas, v_div_fixup).  Checked exhaustively on the MI355X over every
 // normal float of both signs (tools/rcp_check.hip, profiles/r04/rcp_check.json):
 // the only differences are the 2 x (2^24 - 1) x with |x| > 2^126, whose
-// reciprocal is subnormal.  Callers pass values inside the range (inverse
-// depths in [1/far, 1/near]); the `_any` form checks it and divides outside
-// (clip w, determinants).  CSG_FAST_RCP=0 builds the division everywhere (A/B).
+// reciprocal is subnormal.  k_raster's inverse depths lie in [1/far, 1/near],
+// inside the range.  (k_setup keeps the division for clip w and determinants:
+// with a range check and the division as fallback it measured 3% slower,
+// profiles/r04/ab/rcp_packed_smallcover.txt.)  CSG_FAST_RCP=0 builds the
+// division (A/B).
 #ifndef CSG_FAST_RCP
 #define CSG_FAST_RCP 1
 #endif
@@ -87,11 +89,6 @@ __device__ __forceinline__ float rcp_ieee(float x) {
 #else
   return 1.0f / x;
 #endif
-}
-__device__ __forceinline__ float rcp_ieee_any(float x) {
-  float r = rcp_ieee(x);
-  if (!(fabsf(x) >= 0x1p-126f && fabsf(x) <= 0x1p126f)) r = 1.0f / x;   // zero, denormal, huge, inf, NaN
-  return r;
 }
 
 struct Cv3 { float x, y, w; };
@@ -113,7 +110,7 @@ __device__ __forceinline__ void hom_setup(const Cv3* v, Hom& h) {
   }
   const float det = (v[0].x * h.A[0] + v[0].y * h.B[0]) + v[0].w * h.C[0];
   h.ok = det != 0.0f;
-  h.invdet = h.ok ? rcp_ieee_any(det) : 0.0f;
+  h.invdet = h.ok ? 1.0f / det : 0.0f;
 }
 
 // Screen-space planes of the original triangle (spec §3.5-6), from its
@@ -585,7 +582,7 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
       auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
         // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c)
         float su[3], sv[3];
-        const float ra = rcp_ieee_any(a.w), rb = rcp_ieee_any(bb.w), rc = rcp_ieee_any(cc.w);
+        const float ra = 1.0f / a.w, rb = 1.0f / bb.w, rc = 1.0f / cc.w;
         su[0] = a.x * ra; sv[0] = a.y * ra;
         su[1] = bb.x * rb; sv[1] = bb.y * rb;
         su[2] = cc.x * rc; sv[2] = cc.y * rc;
