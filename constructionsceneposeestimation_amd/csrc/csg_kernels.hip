@@ -157,24 +157,6 @@ __device__ __forceinline__ int wrap_index(float fu, int n) {
   return (int)r;
 }
 
-// Both wrapped indices; one branch for the usual case of both coordinates
-// inside one repeat (wrap_index's own test per coordinate made two divergent
-// branches).  CSG_WRAP_PAIR=0: one wrap_index per coordinate (A/B).
-#ifndef CSG_WRAP_PAIR
-#define CSG_WRAP_PAIR 1
-#endif
-__device__ __forceinline__ void wrap_pair(float fu, float fv, int tw, int th, int& x, int& y) {
-#if CSG_WRAP_PAIR
-  if (fu >= 0.0f && fu < (float)tw && fv >= 0.0f && fv < (float)th) {
-    x = (int)fu;
-    y = (int)fv;
-    return;
-  }
-#endif
-  x = wrap_index(fu, tw);
-  y = wrap_index(fv, th);
-}
-
 // Texel coordinates (u * tw - 0.5, (1 - v) * th - 0.5) as one packed multiply and add
 __device__ __forceinline__ f32x2 texel_coords(float u, float v, int tw, int th) {
   const f32x2 a = {u, 1.0f - v}, n = {(float)tw, (float)th};
@@ -194,9 +176,7 @@ __device__ __forceinline__ TexTap tex_taps(int tw, int th, float u, float v) {  
   t.wx = (int)((tu - fu) * 256.0f) & 255;
   t.wy = (int)((tv - fv) * 256.0f) & 255;
   tw &= 0x7FFF;
-  int xw, yw;
-  wrap_pair(fu, fv, tw, th, xw, yw);
-  const int x0 = xw & 0x3FFF, y0 = yw & 0x3FFF;
+  const int x0 = wrap_index(fu, tw) & 0x3FFF, y0 = wrap_index(fv, th) & 0x3FFF;
   const int x1 = (x0 + 1 == tw) ? 0 : x0 + 1;
   const int y1 = (y0 + 1 == th) ? 0 : y0 + 1;
   const uint32_t r0 = __umul24((uint32_t)y0, (uint32_t)tw), r1 = __umul24((uint32_t)y1, (uint32_t)tw);
@@ -248,10 +228,8 @@ __device__ __forceinline__ bool alpha_pass(const uint32_t* aquad, const uint32_t
   if (!(fabsf(tu) < 8388608.0f)) tu = 0.0f;
   if (!(fabsf(tv) < 8388608.0f)) tv = 0.0f;
   const float fu = floorf(tu), fv = floorf(tv);
-  int xw, yw;
-  wrap_pair(fu, fv, tw, th, xw, yw);
-  const uint32_t idx = offset + __umul24((uint32_t)yw & 0x3FFFu, (uint32_t)tw & 0x7FFFu) +
-                       ((uint32_t)xw & 0x3FFFu);   // (masks: see tex_taps)
+  const uint32_t idx = offset + __umul24((uint32_t)wrap_index(fv, th) & 0x3FFFu, (uint32_t)tw & 0x7FFFu) +
+                       ((uint32_t)wrap_index(fu, tw) & 0x3FFFu);   // (masks: see tex_taps)
   const uint32_t cl = (acls[idx >> 4] >> (2u * (idx & 15u))) & 3u;
   if (cl != 3u) return cl != 0u;
   const int wx = (int)((tu - fu) * 256.0f) & 255, wy = (int)((tv - fv) * 256.0f) & 255;
