@@ -58,6 +58,7 @@ DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 10, 2, 2880
 # outputs per frame) take 480 frames per step (240 -> 6.30k, 480 -> 6.34k
 # frames/s): ~115 GB of outputs and ~28 GB of work per rank.
 LARGE_FRAME_PIXELS, LARGE_FRAMES_PER_STEP = 1920 * 1080, 480
+MAX_SETS = 65536   # transform sets per context (kMaxSets, csg_api.cpp)
 
 
 def default_frames_per_step(width: int, height: int) -> int:
@@ -335,6 +336,9 @@ def main():
     # ---- schedule for every step, uploaded before timing -------------------
     fids = rank_frames(rank, world, W + K, F)
     epochs = sorted({f // 10 for f in fids})
+    if len(epochs) > MAX_SETS:
+        raise SystemExit(f"bench: {len(epochs)} randomisation epochs on rank {rank}, the library holds {MAX_SETS} "
+                         "transform sets: fewer --steps or --frames-per-step")
     set_of = {e: i for i, e in enumerate(epochs)}
     NC = max(1, args.contexts)
     ctxs = [Renderer(wl.scene, Wd, H, max_frames=F, device=local, frames_per_launch=args.frames_per_launch)
@@ -355,10 +359,12 @@ def main():
     fsz = FRAME_DTYPE.itemsize
     Kp = r.n_kp
     # Work buffers sized by a sizing pass over this rank's whole schedule (setup
-    # and binning kernels only, outside the timed region): caps = the largest
-    # per-frame record / bin-entry counts x 1.25, so no batch can overflow
-    # (the counts are a pure function of the frame); without it the library
-    # sizes them for every scene triangle per frame (~100 GB at C3 x 960 frames)
+    # and binning kernels only, outside the timed region): each frame record
+    # gets its measured record / bin-entry counts x 1.25 as hints, and the
+    # record and bin pools hold the heaviest run of F consecutive frames, so no
+    # step can overflow (the counts are a pure function of the frame); without
+    # it the library sizes every frame for every scene triangle (~100 GB at C3 x
+    # 960 frames)
     winfo = None
     if args.size_work:
         for c in ctxs:
@@ -627,13 +633,16 @@ def main():
             "with_label_stats": with_stats,
             "stage_ms_per_step": {k: round(tm[k] / K, 4) for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")},
             "work": {"bytes": int(winfo["work_bytes"]), "contexts": NC,
+                     "pool_records": int(winfo["pool_records"]), "pool_bins": int(winfo["pool_bins"]),
+                     "hinted": bool(winfo["hinted"]),
                      "records_per_frame_cap": int(winfo["records_per_frame"]),
                      "bins_per_frame_cap": int(winfo["bins_per_frame"]),
                      "frames_per_launch": int(winfo["frames_per_launch"]),
                      "sized_frames": int(winfo["sized_frames"]), "max_records": int(winfo["max_records"]),
                      "max_bins": int(winfo["max_bins"]), "mean_records": round(winfo["mean_records"], 1),
                      "mean_bins": round(winfo["mean_bins"], 1),
-                     "how": (f"csg_size_work over the rank's {len(fids)} scheduled frames, margin {args.work_margin}"
+                     "how": (f"csg_size_work over the rank's {len(fids)} scheduled frames, margin {args.work_margin}: "
+                             "per-frame hints, pools for the heaviest run of frames_per_launch frames"
                              if args.size_work else "full-scene caps (1.125 x triangles per frame)")},
             "records_per_frame": round(bst["records"] / max(bst["frames"], 1), 1),
             "bin_entries_per_frame": round(bst["bin_entries"] / max(bst["frames"], 1), 1),

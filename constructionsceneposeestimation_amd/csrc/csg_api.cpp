@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -52,6 +53,11 @@ struct DevBuf {
 // keeping records in the Infinity Cache does not pay that back.  Smaller
 // chains only bound the work-buffer memory.
 constexpr uint32_t kAutoChainFrames = 0xFFFFFFFFu;
+
+// Transform / keypoint / randomisation sets per context (ids 0..kMaxSets-1;
+// the tables hold max id + 1 sets).  The bench's default run at 2,880
+// frames per step uses 7,200 epochs on one rank.
+constexpr uint32_t kMaxSets = 65536;
 
 struct HostTexture {
   std::vector<uint8_t> rgba;
@@ -106,8 +112,15 @@ struct csg_ctx {
   DevBuf<float> kp;
   bool kp_dirty = true;
 
-  // per-batch work buffers
+  // per-batch work buffers: record and bin pools shared by the frames of a
+  // launch chain, each frame's region (Slab) planned by k_plan from its hints
+  // or the per-frame caps rec_cap / bin_cap
   uint32_t rec_cap = 0, bin_cap = 0, work_frames = 0;
+  uint64_t rec_pool = 0, bin_pool = 0;            // pool entries allocated
+  bool use_hints = false;                         // csg_size_work sized the pools from frame hints
+  uint64_t plan_rec_pool = 0, plan_bin_pool = 0;  // ... to these
+  DevBuf<Slab> slab;                              // [chain frames] (k_plan)
+  DevBuf<uint64_t> plan_need;                     // [2] pool entries the last chain asked for
   DevBuf<FrameDev> frames;
   // Pinned staging ring for host frame records: a batch's records are copied
   // into the next slot, and a slot is reused only after the H2D copy that read
@@ -490,7 +503,7 @@ int csg_set_light(csg_ctx* c, const csg_light* L) {
 
 int csg_set_dr_light(csg_ctx* c, uint32_t set_id, const csg_light* L) {
   if (!c) return CSG_ERR_INVALID;
-  if (!L || set_id >= 4096) return c->fail(CSG_ERR_INVALID, "set_dr_light: need a light and set < 4096");
+  if (!L || set_id >= kMaxSets) return c->fail(CSG_ERR_INVALID, "set_dr_light: need a light and set < %u", kMaxSets);
   if (c->dr_light_valid.size() <= set_id) {
     c->dr_light_valid.resize(set_id + 1, 0);
     c->dr_light.resize(set_id + 1);
@@ -504,8 +517,8 @@ int csg_set_dr_light(csg_ctx* c, uint32_t set_id, const csg_light* L) {
 int csg_set_dr_textures(csg_ctx* c, uint32_t set_id, const int32_t* tex, uint32_t n) {
   if (!c) return CSG_ERR_INVALID;
   if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "set_dr_textures: no scene");
-  if (!tex || n != c->n_materials || set_id >= 4096)
-    return c->fail(CSG_ERR_INVALID, "set_dr_textures: need %u entries, set < 4096", c->n_materials);
+  if (!tex || n != c->n_materials || set_id >= kMaxSets)
+    return c->fail(CSG_ERR_INVALID, "set_dr_textures: need %u entries, set < %u", c->n_materials, kMaxSets);
   for (uint32_t m = 0; m < n; ++m)
     if (tex[m] < CSG_KEEP_TEXTURE || tex[m] >= 4096)
       return c->fail(CSG_ERR_INVALID, "set_dr_textures: material %u: bad texture id %d", m, tex[m]);
@@ -519,8 +532,8 @@ int csg_set_dr_textures(csg_ctx* c, uint32_t set_id, const int32_t* tex, uint32_
 int csg_set_instance_transforms(csg_ctx* c, uint32_t set_id, const float* model4x4, uint32_t n) {
   if (!c) return CSG_ERR_INVALID;
   if (!c->have_scene) return c->fail(CSG_ERR_INVALID, "set_instance_transforms: no scene");
-  if (!model4x4 || n != c->n_inst || set_id >= 4096)
-    return c->fail(CSG_ERR_INVALID, "set_instance_transforms: need %u matrices, set < 4096", c->n_inst);
+  if (!model4x4 || n != c->n_inst || set_id >= kMaxSets)
+    return c->fail(CSG_ERR_INVALID, "set_instance_transforms: need %u matrices, set < %u", c->n_inst, kMaxSets);
   const size_t per = (size_t)c->n_inst * 16;
   if (c->set_valid.size() <= set_id) {
     c->set_valid.resize(set_id + 1, 0);
@@ -534,7 +547,7 @@ int csg_set_instance_transforms(csg_ctx* c, uint32_t set_id, const float* model4
 
 int csg_set_keypoints(csg_ctx* c, uint32_t set_id, const float* pts, uint32_t n) {
   if (!c) return CSG_ERR_INVALID;
-  if (!pts || set_id >= 4096 || n == 0) return c->fail(CSG_ERR_INVALID, "set_keypoints: bad arguments");
+  if (!pts || set_id >= kMaxSets || n == 0) return c->fail(CSG_ERR_INVALID, "set_keypoints: bad arguments");
   if (c->n_kp && n != c->n_kp) return c->fail(CSG_ERR_INVALID, "set_keypoints: K must stay %u", c->n_kp);
   c->n_kp = n;
   if (c->kp_valid.size() <= set_id) {
@@ -704,24 +717,42 @@ static uint32_t full_record_cap(const csg_ctx* c) {
   return (uint32_t)((n + 3u) & ~3ull);
 }
 
-// Device bytes ensure_work allocates for a launch chain of F frames at the given caps.
-static uint64_t work_bytes_for(const csg_ctx* c, uint64_t F, uint64_t rec_cap, uint64_t bin_cap) {
-  const uint64_t per_frame = rec_cap * (sizeof(Rec) + 4) + bin_cap * 4 +
-                             (uint64_t)c->n_tiles * 4 * (2 + c->bin_blocks) + 4 + (uint64_t)c->n_inst * 12 * 4 +
-                             12 * 4 + kCamFloats * 4 + kCounterStride * 4 + 4;
-  return F * per_frame + (uint64_t)c->cfg.max_frames * sizeof(FrameDev);
+// Device bytes ensure_work allocates for a launch chain of F frames with
+// pools of the given entries.
+static uint64_t work_bytes_for(const csg_ctx* c, uint64_t F, uint64_t rec_pool, uint64_t bin_pool) {
+  const uint64_t per_frame = (uint64_t)c->n_tiles * 4 * (2 + c->bin_blocks) + 4 + (uint64_t)c->n_inst * 12 * 4 +
+                             12 * 4 + kCamFloats * 4 + kCounterStride * 4 + 4 + sizeof(Slab);
+  return rec_pool * (sizeof(Rec) + 4) + bin_pool * 4 + F * per_frame +
+         (uint64_t)c->cfg.max_frames * sizeof(FrameDev);
 }
 
 static void release_work(csg_ctx* c) {
   c->recs.release(); c->rect.release(); c->bins.release(); c->bcount.release();
   c->tile_count.release(); c->tile_off.release(); c->rec_count.release();
-  c->clip.release(); c->pv.release(); c->cam.release(); c->fset.release();
+  c->clip.release(); c->pv.release(); c->cam.release(); c->fset.release(); c->slab.release();
   c->work_frames = 0;
+  c->rec_pool = c->bin_pool = 0;
+}
+
+// Pools a launch chain of F frames gets: sized from the frame hints by
+// csg_size_work, else F frames at the per-frame caps.
+static void target_pools(const csg_ctx* c, uint32_t F, uint64_t& rp, uint64_t& bp) {
+  if (c->use_hints) {
+    rp = c->plan_rec_pool;
+    bp = c->plan_bin_pool;
+  } else {
+    rp = (uint64_t)F * c->rec_cap;
+    bp = (uint64_t)F * ((c->bin_cap + 3u) & ~3u);
+  }
 }
 
 static int ensure_work(csg_ctx* c) {
   const uint32_t maxF = c->chain_frames;   // work buffers hold one launch chain
-  if (c->work_frames == maxF && c->rec_cap && c->bin_cap) return CSG_OK;
+  if (c->rec_cap && c->bin_cap && c->work_frames == maxF) {
+    uint64_t rp, bp;
+    target_pools(c, maxF, rp, bp);
+    if (rp == c->rec_pool && bp == c->bin_pool) return CSG_OK;
+  }
   {  // buffers are reallocated below
     const int rc = drain(c);
     if (rc) return rc;
@@ -731,7 +762,12 @@ static int ensure_work(csg_ctx* c) {
   if (!c->bin_cap)
     c->bin_cap = c->cfg.bins_per_frame ? c->cfg.bins_per_frame
                                        : (uint32_t)std::min<uint64_t>(3ull * c->rec_cap + 16ull * c->n_tiles,
-                                                                      0x7FFFFFFFull);
+                                                                      0x7FFFFFFCull);
+  uint64_t rp, bp;
+  target_pools(c, maxF, rp, bp);
+  if (rp != c->rec_pool || bp != c->bin_pool) {   // DevBuf keeps a larger buffer: release to shrink
+    c->recs.release(); c->rect.release(); c->bins.release();
+  }
   HIP_TRY(c, c->frames.alloc(c->cfg.max_frames));   // the whole batch's frame records
   for (uint32_t k = 0; k < csg_ctx::kStaging; ++k)
     if (!c->h_stage[k])
@@ -740,13 +776,18 @@ static int ensure_work(csg_ctx* c) {
   HIP_TRY(c, c->clip.alloc((size_t)maxF * c->n_inst * 12));
   HIP_TRY(c, c->pv.alloc((size_t)maxF * 12));
   HIP_TRY(c, c->cam.alloc((size_t)maxF * kCamFloats));
-  HIP_TRY(c, c->recs.alloc((size_t)maxF * c->rec_cap));
-  HIP_TRY(c, c->rect.alloc((size_t)maxF * c->rec_cap));
+  c->rec_pool = c->bin_pool = 0;
+  HIP_TRY(c, c->recs.alloc(rp));
+  HIP_TRY(c, c->rect.alloc(rp));
+  HIP_TRY(c, c->bins.alloc(bp));
+  c->rec_pool = rp;
+  c->bin_pool = bp;
   HIP_TRY(c, c->rec_count.alloc((size_t)maxF * kCounterStride));
   HIP_TRY(c, c->tile_count.alloc((size_t)maxF * c->n_tiles));
   HIP_TRY(c, c->tile_off.alloc((size_t)maxF * (c->n_tiles + 1)));
-  HIP_TRY(c, c->bins.alloc((size_t)maxF * c->bin_cap));
   HIP_TRY(c, c->bcount.alloc((size_t)maxF * c->bin_blocks * c->n_tiles));
+  HIP_TRY(c, c->slab.alloc(maxF));
+  HIP_TRY(c, c->plan_need.alloc(2));
   c->work_frames = maxF;
   return CSG_OK;
 }
@@ -820,14 +861,13 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   b.cam = c->cam.p;
   b.recs = c->recs.p;
   b.rect = c->rect.p;
-  b.rec_cap = c->rec_cap;
+  b.slab = c->slab.p;
   b.rec_count = c->rec_count.p;
   b.tile_count = c->tile_count.p;
   b.bcount = c->bcount.p;
   b.bin_blocks = c->bin_blocks;
   b.tile_off = c->tile_off.p;
   b.bins = c->bins.p;
-  b.bin_cap = c->bin_cap;
   b.overflow = c->overflow.p;
   b.n_labels = out->n_labels;
   b.dbg = c->dbg;
@@ -946,6 +986,8 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       ++c->ring_count;
     }
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[0], st));
+    launch_plan(bc.frames, Fc, c->rec_cap, (c->bin_cap + 3u) & ~3u, c->rec_pool, c->bin_pool, c->use_hints ? 1 : 0,
+                c->slab.p, c->plan_need.p, st);
     launch_clip(s, bc, Fc, st);
     launch_setup(s, bc, c->chunks.p, c->n_chunks, Fc, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
@@ -1112,6 +1154,14 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (ov & (kOvBadSet | kOvBadKpSet))   // host frames are validated before launch: cannot happen
       return c->fail(CSG_ERR_DEVICE, "render: unexpected set error flags %u", ov);
+    // Pools planned from frame hints (csg_size_work) overflowed: stale hints
+    // (scene edits after sizing), unmeasured frames, or another grouping of
+    // frames into chains than the sizing assumed.  First retry: no hints, every
+    // frame at the per-frame caps (the largest measured counts with the margin).
+    if (c->use_hints) {
+      c->use_hints = false;
+      continue;
+    }
     // grow the overflowed capacity and re-render (results are a pure function
     // of inputs): at least double it, or size it from the last launch chain's
     // counters (records counted past the cap; bin totals of the records kept)
@@ -1169,11 +1219,13 @@ int csg_get_batch_stats(csg_ctx* c, csg_batch_stats* st) {
   st->frames = F;
   if (!F) return CSG_OK;
   std::vector<uint32_t> rcs((size_t)F * kCounterStride), rc(F), to((size_t)F * (c->n_tiles + 1));
+  std::vector<Slab> sl(F);
   HIP_TRY(c, hipMemcpy(rcs.data(), c->rec_count.p, rcs.size() * 4, hipMemcpyDeviceToHost));
   for (uint32_t f = 0; f < F; ++f) rc[f] = rcs[(size_t)f * kCounterStride];
   HIP_TRY(c, hipMemcpy(to.data(), c->tile_off.p, to.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(sl.data(), c->slab.p, sl.size() * sizeof(Slab), hipMemcpyDeviceToHost));
   for (uint32_t f = 0; f < F; ++f) {
-    st->records += std::min(rc[f], c->rec_cap);
+    st->records += std::min(rc[f], sl[f].rec_cap);
     st->bin_entries += to[(size_t)f * (c->n_tiles + 1) + c->n_tiles];
   }
   if (c->timing) {
@@ -1250,6 +1302,8 @@ static int measure_work(csg_ctx* c, const csg_frame* frames, uint32_t n, bool on
     HIP_TRY(c, c->tile_count.alloc((size_t)P * c->n_tiles));
     HIP_TRY(c, c->tile_off.alloc((size_t)P * (c->n_tiles + 1)));
     HIP_TRY(c, c->bcount.alloc((size_t)P * c->bin_blocks * c->n_tiles));
+    HIP_TRY(c, c->slab.alloc(P));
+    HIP_TRY(c, c->plan_need.alloc(2));
     uint32_t worst = 0;
     for (uint32_t c0 = 0; c0 < n; c0 += P) {
       const uint32_t Fc = std::min(P, n - c0);
@@ -1275,17 +1329,19 @@ static int measure_work(csg_ctx* c, const csg_frame* frames, uint32_t n, bool on
       b.cam = c->cam.p;
       b.recs = c->recs.p;
       b.rect = c->rect.p;
-      b.rec_cap = cap;
+      b.slab = c->slab.p;
       b.rec_count = c->rec_count.p;
       b.tile_count = c->tile_count.p;
       b.bcount = c->bcount.p;
       b.bin_blocks = c->bin_blocks;
       b.tile_off = c->tile_off.p;
-      b.bin_cap = 0x7FFFFFFFu;
       b.overflow = c->overflow.p;
       b.dbg = c->dbg;
       b.tile_words = (c->n_tiles + 31u) / 32u;
       HIP_TRY(c, hipMemsetAsync(c->rec_count.p, 0, sizeof(uint32_t) * Fc * kCounterStride, st));
+      // uniform slabs at the probe cap; no bin cap (no bin pool: k_bin is not run)
+      launch_plan(df, Fc, cap, 0x7FFFFFFCu, (uint64_t)P * cap, (uint64_t)P * 0x7FFFFFFCull, 0, c->slab.p,
+                  c->plan_need.p, st);
       launch_clip(s, b, Fc, st);
       launch_setup(s, b, c->chunks.p, c->n_chunks, Fc, st);
       launch_count(s, b, Fc, c->bin_blocks, st);
@@ -1328,7 +1384,7 @@ static void fill_work_info(const csg_ctx* c, csg_work_info* out) {
   const uint32_t bin = c->bin_cap ? c->bin_cap
                                   : (c->cfg.bins_per_frame ? c->cfg.bins_per_frame
                                                            : (uint32_t)std::min<uint64_t>(3ull * rec + 16ull * c->n_tiles,
-                                                                                          0x7FFFFFFFull));
+                                                                                          0x7FFFFFFCull));
   out->records_per_frame = rec;
   out->bins_per_frame = bin;
   out->frames_per_launch = c->chain_frames;
@@ -1337,10 +1393,36 @@ static void fill_work_info(const csg_ctx* c, csg_work_info* out) {
   out->max_bins = c->sized_max_bin;
   out->mean_records = c->sized_mean_rec;
   out->mean_bins = c->sized_mean_bin;
-  out->work_bytes = work_bytes_for(c, c->chain_frames, rec, bin);
+  if (c->use_hints) {
+    out->pool_records = c->plan_rec_pool;
+    out->pool_bins = c->plan_bin_pool;
+  } else {
+    out->pool_records = (uint64_t)c->chain_frames * ((rec + 3u) & ~3u);
+    out->pool_bins = (uint64_t)c->chain_frames * ((bin + 3u) & ~3u);
+  }
+  out->hinted = c->use_hints ? 1u : 0u;
+  out->work_bytes = work_bytes_for(c, c->chain_frames, out->pool_records, out->pool_bins);
 }
 
-int csg_size_work(csg_ctx* c, const csg_frame* frames, uint32_t n, int32_t frames_on_device, float margin,
+// Largest sum of `w` consecutive entries of v (all of v, plus (w - n) x fill,
+// when v is shorter than a window).
+static uint64_t max_window_sum(const std::vector<uint32_t>& v, uint32_t w, uint32_t fill) {
+  const size_t n = v.size();
+  if (n <= w) {
+    uint64_t t = (uint64_t)(w - n) * fill;
+    for (uint32_t x : v) t += x;
+    return t;
+  }
+  uint64_t run = 0, best = 0;
+  for (size_t i = 0; i < n; ++i) {
+    run += v[i];
+    if (i >= w) run -= v[i - w];
+    if (i + 1 >= w) best = std::max(best, run);
+  }
+  return best;
+}
+
+int csg_size_work(csg_ctx* c, csg_frame* frames, uint32_t n, int32_t frames_on_device, float margin,
                   csg_work_info* out) {
   if (!c) return CSG_ERR_INVALID;
   if (!frames || n == 0 || !(margin >= 0.0f) || margin > 64.0f)
@@ -1368,15 +1450,38 @@ int csg_size_work(csg_ctx* c, const csg_frame* frames, uint32_t n, int32_t frame
     sr += rn[f];
     sb += bn[f];
   }
-  const double k = 1.0 + (double)margin;
-  c->rec_cap = (uint32_t)std::min<uint64_t>((((uint64_t)std::ceil(mr * k) + 256 + 3) & ~3ull), 0x7FFFFFF0ull);
-  c->bin_cap = (uint32_t)std::min<uint64_t>((uint64_t)std::ceil(mb * k) + 1024, 0x7FFFFFFFull);
+  // per-frame caps for unmeasured frames: the largest measured counts
+  c->rec_cap = hinted_cap(mr, margin, 256);
+  c->bin_cap = hinted_cap(mb, margin, 1024);
+  // per-frame hints, written into the frame records: k_plan packs each
+  // chain's frames back to back at these sizes
+  std::vector<uint32_t> rh(n), bh(n);
+  for (uint32_t f = 0; f < n; ++f) {
+    rh[f] = hinted_cap(rn[f], margin, 256);
+    bh[f] = hinted_cap(bn[f], margin, 1024);
+  }
+  if (frames_on_device) {
+    std::vector<uint32_t> pairs((size_t)2 * n);
+    for (uint32_t f = 0; f < n; ++f) { pairs[2 * f] = rh[f]; pairs[2 * f + 1] = bh[f]; }
+    HIP_TRY(c, hipMemcpy2DAsync(reinterpret_cast<uint8_t*>(frames) + offsetof(csg_frame, records_hint),
+                                sizeof(csg_frame), pairs.data(), 8, 8, n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  } else {
+    for (uint32_t f = 0; f < n; ++f) {
+      frames[f].records_hint = rh[f];
+      frames[f].bins_hint = bh[f];
+    }
+  }
+  // pools: the heaviest run of chain_frames consecutive frames of this order
+  c->plan_rec_pool = max_window_sum(rh, c->chain_frames, c->rec_cap);
+  c->plan_bin_pool = max_window_sum(bh, c->chain_frames, (c->bin_cap + 3u) & ~3u);
+  c->use_hints = true;
   c->sized_frames = n;
   c->sized_max_rec = mr;
   c->sized_max_bin = mb;
   c->sized_mean_rec = sr / n;
   c->sized_mean_bin = sb / n;
-  release_work(c);   // the next batch allocates the work buffers at these caps
+  release_work(c);   // the next batch allocates the pools at these sizes
   if (out) fill_work_info(c, out);
   return CSG_OK;
 }

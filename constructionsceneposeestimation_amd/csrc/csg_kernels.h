@@ -79,7 +79,20 @@ struct FrameDev {                // csg_frame mirror
   float proj[16];
   uint32_t xform_set;
   uint32_t frame_id;
+  uint32_t records_hint;         // raster records measured by csg_size_work (0: not measured)
+  uint32_t bins_hint;            // tile-bin entries measured likewise
 };
+
+// A frame's region of the launch chain's record and bin pools (k_plan): the
+// records [rec_base, rec_base + rec_cap) of `recs` / `rect`, the bin entries
+// [bin_base, bin_base + bin_cap) of `bins`.  Bases are multiples of 4 records
+// (16-B aligned rect rows: k_count / k_bin load 4 at once).
+struct Slab {
+  uint64_t rec_base, bin_base;
+  uint32_t rec_cap, bin_cap;
+  uint32_t pad[2];
+};
+static_assert(sizeof(Slab) == 32, "Slab layout");
 
 // Geometry is stored de-indexed ("triangle soup"): the authored vertex and
 // index arrays are expanded at upload so a triangle is one contiguous 36-B
@@ -107,8 +120,8 @@ struct SceneDev {
 };
 
 // Bits of overflow[0] (sticky until csg_synchronize / csg_render_batch reads them)
-constexpr uint32_t kOvRecords = 1u;      // a frame emitted more raster records than rec_cap
-constexpr uint32_t kOvBins = 2u;         // a frame's tile-bin entries exceeded bin_cap
+constexpr uint32_t kOvRecords = 1u;      // a frame emitted more raster records than its slab holds
+constexpr uint32_t kOvBins = 2u;         // a frame's tile-bin entries exceeded its slab
 constexpr uint32_t kOvBadSet = 4u;       // device frame named a transform set >= n_sets (rendered with set 0)
 constexpr uint32_t kOvBadKpSet = 8u;     // device frame named a keypoint set >= n_kp_sets (keypoints vis 0)
 
@@ -124,14 +137,13 @@ struct BatchDev {
   uint32_t n_mat;
   float* clip;                 // [F][I][12] rows 0,1,3 of P*V*M
   float* pv;                   // [F][12]    rows 0,1,3 of P*V
-  Rec* recs;                   // [F][rec_cap]
-  uint32_t* rect;              // [F][rec_cap] tile rect tx0|ty0<<8|tx1<<16|ty1<<24
-  uint32_t rec_cap;
+  Rec* recs;                   // record pool: frame f's records at slab[f].rec_base
+  uint32_t* rect;              // same indexing: tile rect tx0|ty0<<8|tx1<<16|ty1<<24
+  const Slab* slab;            // [F] each frame's region of the pools (k_plan)
   uint32_t* rec_count;         // [F * kCounterStride] (one cache line per frame: no atomic contention)
   uint32_t* tile_count;        // [F][n_tiles] (k_colscan)
   uint32_t* tile_off;          // [F][n_tiles+1]
-  uint32_t* bins;              // [F][bin_cap]
-  uint32_t bin_cap;
+  uint32_t* bins;              // bin pool: frame f's tile lists at slab[f].bin_base (tile_off relative to it)
   uint32_t* bcount;            // [F][bin_blocks][n_tiles]: each k_count block's tile counts,
                                //   then (k_colscan) the block's first slot in each tile's list, tile-relative
   uint32_t bin_blocks;
@@ -160,6 +172,18 @@ struct BatchDev {
 };
 
 // launchers (all enqueue on `st`)
+// k_plan: each frame's slab from its hints (use_hints; 0 = none) or the
+// default caps, packed back to back; frames past a pool's end get what is
+// left (possibly nothing: they overflow).  need[0], need[1]: the pool
+// entries the chain asked for.  Pools are multiples of 4 entries.
+void launch_plan(const FrameDev* frames, uint32_t F, uint32_t def_rec, uint32_t def_bin, uint64_t rec_pool,
+                 uint64_t bin_pool, int use_hints, Slab* slab, uint64_t* need, hipStream_t st);
+// csg_size_work's hint for a measured count: count x (1 + margin) + pad, 4-aligned, < 2^31
+inline uint32_t hinted_cap(uint32_t count, double margin, uint32_t pad) {
+  const double c = (double)count * (1.0 + margin);
+  const uint64_t v = (uint64_t)c + (c > (double)(uint64_t)c ? 1u : 0u) + pad;
+  return (uint32_t)(((v < 0x7FFFFFF0ull ? v : 0x7FFFFFF0ull) + 3u) & ~3ull);
+}
 void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks,
                   uint32_t F, hipStream_t st);

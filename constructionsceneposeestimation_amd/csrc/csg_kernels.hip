@@ -649,9 +649,11 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   static_assert(16 * kRecGroups <= 2 * 64, "two chunk stores per lane");
   __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
   uint4* sw = tstage[tid >> 6];
-  if (lane == 0 && wbase + wtot > b.rec_cap) atomicOr(b.overflow, 1u);
-  uint4* dst = reinterpret_cast<uint4*>(b.recs + (size_t)f * b.rec_cap);
-  const size_t lim = (size_t)b.rec_cap * kRecGroups;
+  const uint64_t rbase = b.slab[f].rec_base;
+  const uint32_t rcap = b.slab[f].rec_cap;
+  if (lane == 0 && wbase + wtot > rcap) atomicOr(b.overflow, 1u);
+  uint4* dst = reinterpret_cast<uint4*>(b.recs + rbase);
+  const size_t lim = (size_t)rcap * kRecGroups;
   auto put = [&](uint32_t at, const SubRec& r) {
     uint4* o = sw + at * kRecGroups;
     o[0] = r.g0;
@@ -677,8 +679,8 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
-  if (nrec > 0 && wbase + mine < b.rec_cap) b.rect[(size_t)f * b.rec_cap + wbase + mine] = rec_tile_rect(r0);
-  if (nrec > 1 && wbase + mine + 1 < b.rec_cap) b.rect[(size_t)f * b.rec_cap + wbase + mine + 1] = rec_tile_rect(r1);
+  if (nrec > 0 && wbase + mine < rcap) b.rect[rbase + wbase + mine] = rec_tile_rect(r0);
+  if (nrec > 1 && wbase + mine + 1 < rcap) b.rect[rbase + wbase + mine + 1] = rec_tile_rect(r1);
 }
 
 // ---------------------------------------------------------------------------
@@ -722,7 +724,7 @@ __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32
   static_assert(kBinRpt == 4, "one 16-B rect load per thread");
   uint4 v = make_uint4(0u, 0u, 0u, 0u);
   if (r0 + 3 < n) {
-    v = *reinterpret_cast<const uint4*>(rect + r0);   // rect rows are 16-B aligned (rec_cap % 4 == 0)
+    v = *reinterpret_cast<const uint4*>(rect + r0);   // rect rows are 16-B aligned (slab bases % 4 == 0)
   } else {
     if (r0 < n) v.x = rect[r0];
     if (r0 + 1 < n) v.y = rect[r0 + 1];
@@ -763,8 +765,8 @@ __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
   uint32_t* wsum = lrc + kBinRound;                    // [4]
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x;
-  const uint32_t n = min(b.rec_count[f * kCounterStride], b.rec_cap);
-  const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
+  const uint32_t n = min(b.rec_count[f * kCounterStride], b.slab[f].rec_cap);
+  const uint32_t* rect = b.rect + b.slab[f].rec_base;
   for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
   __syncthreads();
   for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
@@ -800,6 +802,55 @@ __global__ __launch_bounds__(256) void k_colscan(SceneDev s, BatchDev b) {
 }
 
 // ---------------------------------------------------------------------------
+// k_plan: each frame's slab of the chain's record and bin pools, packed back
+// to back in frame order.  A frame's caps are its hints (csg_size_work wrote
+// them into the frame record: the measured counts with the margin) or the
+// context's per-frame caps.  One wave: 64 frames per step, a 64-bit
+// inclusive scan over the wave, a running base.  A frame past a pool's end
+// gets what is left (possibly nothing): k_setup / k_scan flag its overflow.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(64) void k_plan(const FrameDev* __restrict__ frames, uint32_t F, uint32_t def_rec,
+                                             uint32_t def_bin, uint64_t rec_pool, uint64_t bin_pool, int use_hints,
+                                             Slab* __restrict__ slab, uint64_t* __restrict__ need) {
+  const int lane = threadIdx.x;
+  uint64_t cr = 0, cb = 0;
+  for (uint32_t f0 = 0; f0 < F; f0 += 64) {
+    const uint32_t f = f0 + (uint32_t)lane;
+    uint32_t rc = 0, bc = 0;
+    if (f < F) {
+      const uint32_t rh = use_hints ? frames[f].records_hint : 0u, bh = use_hints ? frames[f].bins_hint : 0u;
+      rc = rh ? ((min(rh, 0x7FFFFFF0u) + 3u) & ~3u) : def_rec;
+      bc = bh ? ((min(bh, 0x7FFFFFF0u) + 3u) & ~3u) : def_bin;
+    }
+    const uint64_t ir = wave_incl_scan64(rc, lane), ib = wave_incl_scan64(bc, lane);
+    if (f < F) {
+      Slab sl;
+      sl.rec_base = min(cr + ir - rc, rec_pool);
+      sl.bin_base = min(cb + ib - bc, bin_pool);
+      sl.rec_cap = (uint32_t)min((uint64_t)rc, rec_pool - sl.rec_base);
+      sl.bin_cap = (uint32_t)min((uint64_t)bc, bin_pool - sl.bin_base);
+      sl.pad[0] = sl.pad[1] = 0u;
+      slab[f] = sl;
+    }
+    cr += __shfl(ir, 63, 64);
+    cb += __shfl(ib, 63, 64);
+  }
+  if (lane == 0) {
+    need[0] = cr;
+    need[1] = cb;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_scan: per frame exclusive scan of tile counts (one 256-thread block)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_scan(SceneDev s, BatchDev b) {
@@ -823,7 +874,7 @@ __global__ __launch_bounds__(256) void k_scan(SceneDev s, BatchDev b) {
   }
   if (threadIdx.x == 0) {
     to[s.n_tiles] = carry;
-    if (carry > b.bin_cap) atomicOr(b.overflow, 2u);
+    if (carry > b.slab[f].bin_cap) atomicOr(b.overflow, 2u);
   }
 }
 
@@ -841,10 +892,11 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   __shared__ uint32_t wsum[kBlock / 64];
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x;
-  const uint32_t n = min(b.rec_count[f * kCounterStride], b.rec_cap);
-  const uint32_t* rect = b.rect + (size_t)f * b.rec_cap;
+  const Slab sb = b.slab[f];
+  const uint32_t n = min(b.rec_count[f * kCounterStride], sb.rec_cap);
+  const uint32_t* rect = b.rect + sb.rec_base;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
-  uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
+  uint32_t* bins = b.bins + sb.bin_base;
   const uint32_t* bo = b.bcount + ((size_t)f * gridDim.x + blockIdx.x) * s.n_tiles;
   // Reverse append order: this block's range mirrored, filled from its end.
   // Outputs do not depend on the order (the z-buffer minimum and the coverage
@@ -861,7 +913,7 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
     for (uint32_t j = tid; j < total; j += kBlock) {
       const int k = find_bin_item(pre, j);
       const uint32_t slot = atomicSub(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
-      if (slot < b.bin_cap) bins[slot] = base + (uint32_t)k;
+      if (slot < sb.bin_cap) bins[slot] = base + (uint32_t)k;
     }
     __syncthreads();
   }
@@ -1191,11 +1243,12 @@ struct RasterLds {
 // owner map cost a workgroup per CU in LDS).
 template <bool kCov, int NS>
 __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev& s, const BatchDev& b, RasterLds<NS>& L,
-                                             uint32_t beg, uint32_t end, const uint32_t* bins, const Rec* recs) {
+                                             uint32_t beg, uint32_t end, const uint32_t* bins, const Rec* recs,
+                                             uint32_t rec_cap) {
   const int tid = threadIdx.x;
   for (uint32_t base = beg; base < end; base += NS) {
     uint32_t row0;
-    const uint32_t rows = stage_record(recs, bins, base + tid, end, b.rec_cap, L.img, tid, c.ox, c.oy, row0);
+    const uint32_t rows = stage_record(recs, bins, base + tid, end, rec_cap, L.img, tid, c.ox, c.oy, row0);
     if (tid < NS) L.row0[tid] = (uint8_t)row0;
     if constexpr (kCov) {   // label of the staged record (read back from this thread's own slot)
       if (tid < NS) {
@@ -1593,8 +1646,9 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   const uint32_t f = blockIdx.y;
   const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
-  const uint32_t beg = min(toff[tile], b.bin_cap);
-  const uint32_t end = (DBG(b.dbg) & 2u) ? beg : min(toff[tile + 1], b.bin_cap);
+  const Slab sb = b.slab[f];
+  const uint32_t beg = min(toff[tile], sb.bin_cap);
+  const uint32_t end = (DBG(b.dbg) & 2u) ? beg : min(toff[tile + 1], sb.bin_cap);
   if (beg == end && !(DBG(b.dbg) & 2u)) {   // nothing binned here: background only
     empty_tile(s, b, f, tile, ox, oy);
     return;
@@ -1610,12 +1664,12 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     if (tid < kCovSlots) covl.keys[tid] = kNoAlpha;
     if (tid == 0) covl.ovf = 0u;
   }
-  const uint32_t* bins = b.bins + (size_t)f * b.bin_cap;
-  const Rec* recs = b.recs + (size_t)f * b.rec_cap;
+  const uint32_t* bins = b.bins + sb.bin_base;
+  const Rec* recs = b.recs + sb.rec_base;
   RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow, covp, rlabel,
               kCov ? b.covered + (size_t)f * b.n_labels : nullptr};
   __syncthreads();
-  raster_block<kCov, NS>(c, s, b, L.ra.r, beg, end, bins, recs);
+  raster_block<kCov, NS>(c, s, b, L.ra.r, beg, end, bins, recs, sb.rec_cap);
   __syncthreads();
   if constexpr (kCov) {
     // per slot: popcount of its 32 mask words, 8 threads per slot (4 words
@@ -2107,6 +2161,12 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
   const size_t lds = (((s.n_tiles + 3u) & ~3u) + 2 * kBinRound + 12) * sizeof(uint32_t);
   hipLaunchKernelGGL(k_count, dim3(blocks, F), dim3(kBlock), lds, st, s, b);
+}
+
+void launch_plan(const FrameDev* frames, uint32_t F, uint32_t def_rec, uint32_t def_bin, uint64_t rec_pool,
+                 uint64_t bin_pool, int use_hints, Slab* slab, uint64_t* need, hipStream_t st) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, st, frames, F, def_rec, def_bin, rec_pool, bin_pool, use_hints,
+                     slab, need);
 }
 
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {

@@ -21,7 +21,8 @@ from .camera_math import Intrinsics
 from .packing import PackedScene, light_constants, pack_scene
 from .scene.model import Scene
 
-FRAME_DTYPE = np.dtype([("view", "<f4", 16), ("proj", "<f4", 16), ("xform_set", "<u4"), ("frame_id", "<u4")])
+FRAME_DTYPE = np.dtype([("view", "<f4", 16), ("proj", "<f4", 16), ("xform_set", "<u4"), ("frame_id", "<u4"),
+                        ("records_hint", "<u4"), ("bins_hint", "<u4")])
 assert FRAME_DTYPE.itemsize == C.sizeof(_lib.Frame)
 
 OUTPUT_KINDS = ("rgb", "instance", "depth", "keypoints", "stats", "normals", "points", "depth_vis", "depth_range",
@@ -333,9 +334,12 @@ class Renderer:
 
     def size_work(self, frames, n: Optional[int] = None, on_device: bool = False,
                   margin: float = 0.25) -> Dict[str, float]:
-        """Size the per-frame work buffers from a sizing pass over ``frames``
+        """Size the work buffers from a sizing pass over ``frames``
         (csg_size_work): a FRAME_DTYPE array, or with ``on_device`` a device
-        pointer (int) to ``n`` frame records.  Returns :meth:`work_info`."""
+        pointer (int) to ``n`` frame records.  Writes each frame's work hints
+        (``records_hint``, ``bins_hint``) into the records passed -- the array
+        itself, or the device records -- so later batches of those records get
+        regions of their own size.  Returns :meth:`work_info`."""
         info = _lib.WorkInfo()
         if on_device:
             self._check(self.lib.csg_size_work(self.ctx, int(frames), int(n), 1, float(margin), C.byref(info)),
@@ -344,13 +348,16 @@ class Renderer:
             fr = np.ascontiguousarray(frames, FRAME_DTYPE)
             self._check(self.lib.csg_size_work(self.ctx, fr.ctypes.data, fr.shape[0], 0, float(margin),
                                                C.byref(info)), "size_work")
-        return {k: getattr(info, k) for k, _ in _lib.WorkInfo._fields_}
+            if fr is not frames:   # a converted copy: hand the hints back
+                frames["records_hint"] = fr["records_hint"]
+                frames["bins_hint"] = fr["bins_hint"]
+        return {k: getattr(info, k) for k, _ in _lib.WorkInfo._fields_ if k != "pad"}
 
     def work_info(self) -> Dict[str, float]:
         """Current work-buffer caps, the last sizing pass and the buffers' device bytes."""
         info = _lib.WorkInfo()
         self._check(self.lib.csg_get_work_info(self.ctx, C.byref(info)), "get_work_info")
-        return {k: getattr(info, k) for k, _ in _lib.WorkInfo._fields_}
+        return {k: getattr(info, k) for k, _ in _lib.WorkInfo._fields_ if k != "pad"}
 
     def timing_reset(self) -> None:
         self._check(self.lib.csg_timing_reset(self.ctx), "timing_reset")

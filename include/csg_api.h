@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 9
+#define CSG_ABI_VERSION 10
 
 typedef enum {
   CSG_OK = 0,
@@ -114,6 +114,8 @@ typedef struct {
   float proj[16];            /* row-major; rows 0,1,3 give (u*w, v*w, w) in pixels */
   uint32_t xform_set;        /* instance-transform set (randomisation epoch) */
   uint32_t frame_id;
+  uint32_t records_hint;     /* work to reserve for this frame: raster records and tile-bin */
+  uint32_t bins_hint;        /* entries; csg_size_work writes them (0 = the per-frame caps) */
 } csg_frame;
 
 typedef struct {
@@ -189,7 +191,7 @@ int csg_upload_scene(csg_ctx* ctx, const csg_mesh* meshes, uint32_t n_meshes,
 int csg_upload_texture(csg_ctx* ctx, uint32_t tex_id, const uint8_t* rgba8, uint32_t width,
                        uint32_t height);
 int csg_set_light(csg_ctx* ctx, const csg_light* light);
-/* n must equal the scene's instance count; set_id < 4096. */
+/* n must equal the scene's instance count; set_id < 65536 (also for the per-set calls below). */
 int csg_set_instance_transforms(csg_ctx* ctx, uint32_t set_id, const float* model4x4, uint32_t n);
 /* World-space keypoints of one transform set: [n][3]; n is fixed per scene. */
 int csg_set_keypoints(csg_ctx* ctx, uint32_t set_id, const float* pts_world, uint32_t n);
@@ -256,10 +258,12 @@ int csg_copy_files(csg_ctx* ctx, uint8_t* dst, uint64_t cap, uint64_t* offsets);
 int csg_host_alloc(csg_ctx* ctx, uint64_t bytes, void** out);
 int csg_host_free(csg_ctx* ctx, void* p);
 
-/* Work-buffer sizing.  k_setup appends each frame's raster records into a
- * fixed per-frame region of `records_per_frame` records and k_bin its tile
- * lists into `bins_per_frame` entries; the buffers hold one launch chain
- * (frames_per_launch frames).  With the config's caps 0 they are sized for
+/* Work-buffer sizing.  k_setup appends each frame's raster records into the
+ * frame's region of a record pool and k_bin its tile lists into a region of a
+ * bin pool; the pools hold one launch chain (frames_per_launch frames), whose
+ * frames get back-to-back regions (a planning kernel at the head of the
+ * chain).  A frame's region is its csg_frame hints, or with hints 0 the
+ * per-frame caps.  With the config's caps 0 and no sizing those are sized for
  * every triangle of the scene (1.125 x triangles per frame, 3x that in bin
  * entries), which no frame can overflow but which a typical view uses a
  * fraction of (C3 1080p: ~1/5 of the records, ~1/9 of the bin entries).
@@ -267,16 +271,24 @@ int csg_host_free(csg_ctx* ctx, void* p);
  * csg_size_work runs the sizing pass on `n_frames` frames (host records, or
  * device records when frames_on_device = 1; any number, in chains of 64):
  * k_clip, k_setup, k_count, k_colscan and k_scan only, no raster and no
- * outputs; then sets the caps to the largest per-frame record and bin-entry
- * counts among them times (1 + margin) (margin >= 0, e.g. 0.25), and frees
- * the work buffers (the next batch allocates them at the new caps).  The
- * counts are a pure function of the frame, so batches of the measured frames
- * never overflow.  Other frames can: csg_render_batch then grows the caps and
- * renders again; an asynchronous batch reports CSG_ERR_OVERFLOW at the next
- * csg_synchronize.  Waits for the context's earlier batches first (and
- * reports their errors). */
+ * outputs.  It then
+ *   - writes each frame's hints: its measured record and bin-entry counts
+ *     times (1 + margin) (margin >= 0, e.g. 0.25) plus a small pad, into
+ *     the frame records passed (device or host memory);
+ *   - sets the per-frame caps (frames without hints) to the largest counts
+ *     measured, with the same margin;
+ *   - sizes the pools for the heaviest run of frames_per_launch consecutive
+ *     frames of the order given (fewer frames than that: all of them plus
+ *     the rest at the per-frame caps),
+ * and frees the work buffers (the next batch allocates them).  The counts are
+ * a pure function of the frame and the scene, so batches that render the
+ * measured frames, in that order, with their hints, never overflow.  Other
+ * batches can: csg_render_batch then renders again without hints (every frame
+ * at the per-frame caps), then with grown caps; an asynchronous batch reports
+ * CSG_ERR_OVERFLOW at the next csg_synchronize.  Waits for the context's
+ * earlier batches first (and reports their errors). */
 typedef struct {
-  uint32_t records_per_frame;  /* current caps */
+  uint32_t records_per_frame;  /* current per-frame caps (frames without hints) */
   uint32_t bins_per_frame;
   uint32_t frames_per_launch;  /* frames the work buffers hold (one launch chain) */
   uint32_t sized_frames;       /* frames the last csg_size_work measured (0: none) */
@@ -284,9 +296,13 @@ typedef struct {
   uint32_t max_bins;
   double mean_records;         /* and their means */
   double mean_bins;
-  uint64_t work_bytes;         /* device bytes of the work buffers at the current caps */
+  uint64_t work_bytes;         /* device bytes of the work buffers at the current pools */
+  uint64_t pool_records;       /* pool entries of one launch chain */
+  uint64_t pool_bins;
+  uint32_t hinted;             /* 1: pools sized from frame hints (csg_size_work) */
+  uint32_t pad;
 } csg_work_info;
-int csg_size_work(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames, int32_t frames_on_device,
+int csg_size_work(csg_ctx* ctx, csg_frame* frames, uint32_t n_frames, int32_t frames_on_device,
                   float margin, csg_work_info* out);
 int csg_get_work_info(csg_ctx* ctx, csg_work_info* out);
 

@@ -131,3 +131,17 @@ def _shard_worker(rank, port, out_dir):
         json.dump(rep, open(os.path.join(out_dir, "rep.json"), "w"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("steps,warmup", [(20, 5), (10, 2), (200, 10)])
+def test_transform_sets_fit_the_library_for_driver_runs(steps, warmup):
+    """Every randomisation epoch of a rank's schedule takes one transform set:
+    at the default 2,880 frames per step the driver's `--steps 20 --warmup 5`
+    needs 7,200 sets (past round 4's first limit of 4,096); the library holds
+    MAX_SETS and the bench fails early, with a message, beyond that."""
+    F = bench.DEFAULT_FRAMES_PER_STEP
+    fids = bench.rank_frames(0, 1, steps + warmup, F)
+    assert len({f // 10 for f in fids}) <= bench.MAX_SETS
+    src = open(os.path.join(os.path.dirname(bench.__file__), "constructionsceneposeestimation_amd", "csrc",
+                            "csg_api.cpp")).read()
+    assert f"constexpr uint32_t kMaxSets = {bench.MAX_SETS};" in src
