@@ -595,7 +595,9 @@ def main():
             h_vis = torch.empty((F, max(Kp, 1)), dtype=torch.int32, pin_memory=True)
             o = _lib.Outputs(h_rgb.data_ptr(), h_inst.data_ptr(), None, h_uv.data_ptr() if want_kp else None,
                              h_vis.data_ptr() if want_kp else None, None, r.n_labels, 0, None, None)
-            hframes = np.ascontiguousarray(frames[:F])
+            # the first step's records as the device holds them: with their work
+            # hints (csg_size_work wrote those into frames_dev, not `frames`)
+            hframes = frames_dev[:F * fsz].cpu().numpy().view(FRAME_DTYPE)
             r._check(r.lib.csg_render_batch_async(r.ctx, hframes.ctypes.data, F, 0, C.byref(o), None), "pcie")
             r.synchronize()
             t1 = time.perf_counter()

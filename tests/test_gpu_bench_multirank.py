@@ -54,3 +54,27 @@ def test_bench_two_ranks_under_torchrun(tmp_path):
     assert sh["epochs_mod_world"] == [[0], [1]]
     # value = every rank's frames over the slowest rank's time
     assert abs(d["value"] - 2 * steps * F / (d["ms_per_step"] * steps / 1e3)) <= 0.01 * d["value"]
+
+
+@pytest.mark.timeout(600)
+def test_bench_single_rank_every_leg_with_hinted_pools(tmp_path):
+    """N = 1 with two launch chains per step: the sizing pass's hints and
+    chain pools carry the timed steps, the PCIe-inclusive leg (host frame
+    records, host outputs) and the label-statistics leg without overflow."""
+    steps, warmup, F, G = 2, 1, 96, 48
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup", str(warmup),
+           "--frames-per-step", str(F), "--frames-per-launch", str(G), "--verify-frames", "4",
+           "--pcie-steps", "1", "--stats-steps", "1", "--cpu-single-frames", "1"]
+    log = tmp_path / "bench1.err"
+    with open(log, "w") as err:
+        r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=err, text=True, timeout=540)
+    tail = log.read_text()[-4000:]
+    assert r.returncode == 0, f"bench at N=1 failed ({r.returncode}):\n{tail}"
+    assert "failed" not in log.read_text(), tail
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["verified"]["frames"] == 4 and d["verified"]["bit_exact"] is True
+    w = d["work"]
+    assert w["hinted"] is True and w["frames_per_launch"] == G
+    assert w["pool_records"] < G * w["records_per_frame_cap"]
+    assert d["pcie_inclusive"] is not None and d["pcie_inclusive"]["value"] > 0
+    assert d["with_label_stats"] is not None
