@@ -325,6 +325,7 @@ void csg_destroy(csg_ctx* c) {
   c->acls.release();
   c->texd.release(); c->models.release(); c->kp.release(); c->frames.release(); c->clip.release();
   c->pv.release(); c->recs.release(); c->rect.release(); c->rec_count.release(); c->tile_count.release();
+  c->slab.release(); c->plan_need.release();
   c->tile_off.release(); c->bins.release(); c->bcount.release(); c->overflow.release(); c->o_rgb.release();
   c->o_inst.release(); c->o_depth.release(); c->o_kp_uv.release(); c->o_kp_vis.release(); c->o_stats.release();
   c->kp_w.release(); c->kp_pix.release(); c->kp_tiles.release();
