@@ -733,6 +733,7 @@ static void release_work(csg_ctx* c) {
   c->clip.release(); c->pv.release(); c->cam.release(); c->fset.release(); c->slab.release();
   c->work_frames = 0;
   c->rec_pool = c->bin_pool = 0;
+  c->last_F = 0;   // the last chain's counters are gone (csg_get_batch_stats: no frames)
 }
 
 // Pools a launch chain of F frames gets: sized from the frame hints by
