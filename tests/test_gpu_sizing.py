@@ -63,6 +63,7 @@ def test_sized_caps_c3_1080p_async_matches_full_caps():
         assert fr["records_hint"].max() == info["records_per_frame"]
         assert fr["bins_hint"].max() == info["bins_per_frame"]
         assert info["hinted"] == 1
+        assert r.batch_stats()["frames"] == 0          # the sizing pass's chains are not a batch
         assert info["pool_records"] == int(fr["records_hint"].astype(np.int64).sum())   # n <= frames per chain
         assert info["pool_bins"] == int(fr["bins_hint"].astype(np.int64).sum())
         assert info["sized_frames"] == n
