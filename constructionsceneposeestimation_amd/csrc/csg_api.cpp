@@ -274,8 +274,8 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   if (!cfg || !out) return CSG_ERR_INVALID;
   *out = nullptr;
   if (cfg->width == 0 || cfg->height == 0 || cfg->width > 8192 || cfg->height > 8192 || cfg->max_frames == 0 ||
-      !(cfg->near_clip > 0.f) || !(cfg->far_clip > cfg->near_clip))
-    return CSG_ERR_INVALID;
+      !(cfg->near_clip >= 0x1p-126f) || !(cfg->far_clip > cfg->near_clip) || !(cfg->far_clip <= 0x1p126f))
+    return CSG_ERR_INVALID;   // clip distances in [2^-126, 2^126]: the range of rcp_ieee's proof (k_setup, k_raster)
   csg_ctx* c = new csg_ctx();
   c->cfg = *cfg;
   if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);

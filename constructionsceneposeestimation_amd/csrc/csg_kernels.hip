@@ -74,9 +74,12 @@ __device__ __forceinline__ void mat4_mul(const float* a, const float* b, float* 
 // normal float of both signs (tools/rcp_check.hip, profiles/r04/rcp_check.json):
 // the only differences are the 2 x (2^24 - 1) x with |x| > 2^126, whose
 // reciprocal is subnormal.  k_raster's inverse depths lie in [1/far, 1/near],
-// inside the range.  (k_setup keeps the division for clip w and determinants:
-// with a range check and the division as fallback it measured 3% slower,
-// profiles/r04/ab/rcp_packed_smallcover.txt.)  CSG_FAST_RCP=0 builds the
+// inside the range (csg_create keeps near / far clip in [2^-126, 2^126]).
+// k_setup uses it for the per-vertex 1/W (W >= near_clip after near-plane
+// clipping; setup -1.9%, profiles/r04/ab/setup_w_rcp.txt) and keeps the
+// division for determinants and the near-plane crossing (a range-checked
+// reciprocal for all of them measured 3% slower,
+// profiles/r04/ab/rcp_packed_smallcover.txt).  CSG_FAST_RCP=0 builds the
 // division (A/B).
 #ifndef CSG_FAST_RCP
 #define CSG_FAST_RCP 1
@@ -580,9 +583,13 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
         nq = (code == 1 || code == 2 || code == 4) ? 3 : 4;
       }
       auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
-        // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c)
+        // spec 3: one IEEE reciprocal per vertex, u = X * (1/W) (as csg_oracle.c).
+        // W >= near_clip > 2^-126 here (near-plane clipping), so below 2^126
+        // the Newton reciprocal is the IEEE one (rcp_ieee); the division only
+        // past that (never taken by real scenes: a uniform branch)
+        auto rcp_w = [](float w) { return w <= 0x1p126f ? rcp_ieee(w) : 1.0f / w; };
         float su[3], sv[3];
-        const float ra = 1.0f / a.w, rb = 1.0f / bb.w, rc = 1.0f / cc.w;
+        const float ra = rcp_w(a.w), rb = rcp_w(bb.w), rc = rcp_w(cc.w);
         su[0] = a.x * ra; sv[0] = a.y * ra;
         su[1] = bb.x * rb; sv[1] = bb.y * rb;
         su[2] = cc.x * rc; sv[2] = cc.y * rc;

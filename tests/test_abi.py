@@ -43,6 +43,11 @@ def test_invalid_config_rejected_without_gpu():
     assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
     bad = _lib.Config(0, 1920, 1080, 8, 0.5, 0.1, 0, 0)
     assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
+    # clip distances outside [2^-126, 2^126] (the Newton reciprocal's proven range)
+    bad = _lib.Config(0, 1920, 1080, 8, 1e-39, 250.0, 0, 0)
+    assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
+    bad = _lib.Config(0, 1920, 1080, 8, 0.5, 1e38, 0, 0)
+    assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
 
 
 def test_struct_layouts_match_c():
