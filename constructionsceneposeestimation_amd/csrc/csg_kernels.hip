@@ -76,10 +76,11 @@ __device__ __forceinline__ void mat4_mul(const float* a, const float* b, float* 
 // reciprocal is subnormal.  k_raster's inverse depths lie in [1/far, 1/near],
 // inside the range (csg_create keeps near / far clip in [2^-126, 2^126]).
 // k_setup uses it for the per-vertex 1/W (W >= near_clip after near-plane
-// clipping; setup -1.9%, profiles/r04/ab/setup_w_rcp.txt) and keeps the
-// division for determinants and the near-plane crossing (a range-checked
-// reciprocal for all of them measured 3% slower,
-// profiles/r04/ab/rcp_packed_smallcover.txt).  CSG_FAST_RCP=0 builds the
+// clipping; setup -1.9%, profiles/r04/ab/setup_w_rcp.txt) and, range-checked,
+// for 1/det (hom_setup: -0.5%, profiles/r04/ab/det_rcp.txt); the near-plane
+// crossing is a true quotient and stays a division.  (Round 4's first
+// attempt, every k_setup division range-checked at once, measured 3% slower:
+// profiles/r04/ab/rcp_packed_smallcover.txt.)  CSG_FAST_RCP=0 builds the
 // division (A/B).
 #ifndef CSG_FAST_RCP
 #define CSG_FAST_RCP 1
@@ -113,7 +114,9 @@ __device__ __forceinline__ void hom_setup(const Cv3* v, Hom& h) {
   }
   const float det = (v[0].x * h.A[0] + v[0].y * h.B[0]) + v[0].w * h.C[0];
   h.ok = det != 0.0f;
-  h.invdet = h.ok ? 1.0f / det : 0.0f;
+  // 1/det: the Newton reciprocal inside its proven range, the division outside
+  const float ad = fabsf(det);
+  h.invdet = !h.ok ? 0.0f : (ad >= 0x1p-126f && ad <= 0x1p126f) ? rcp_ieee(det) : 1.0f / det;
 }
 
 // Screen-space planes of the original triangle (spec §3.5-6), from its
