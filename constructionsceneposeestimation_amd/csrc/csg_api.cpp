@@ -222,8 +222,9 @@ static int take_flags(csg_ctx* c, uint32_t* flags_out) {
     uint32_t ctr[16];
     HIP_TRY(c, hipMemcpy(ctr, c->overflow.p, sizeof(ctr), hipMemcpyDeviceToHost));
     fprintf(stderr, "[csg] staged_recs %u row_items %u spans %u l2_items %u alpha_fail %u alpha_pass %u early_z %u "
-            "wide_rows %u small_recs %u small_rows %u small_items %u\n", ctr[1], ctr[2], ctr[3], ctr[4], ctr[5],
-            ctr[6], ctr[7], ctr[8], ctr[9], ctr[10], ctr[11]);
+            "wide_rows %u small_recs %u small_rows %u small_items %u alpha_waves %u alpha_wave_lanes %u l2_waves %u "
+            "l2_wave_lanes %u\n", ctr[1], ctr[2], ctr[3], ctr[4], ctr[5], ctr[6], ctr[7], ctr[8], ctr[9], ctr[10],
+            ctr[11], ctr[12], ctr[13], ctr[14], ctr[15]);
   }
   if (flags_out) *flags_out = ov;
   if (!ov) return CSG_OK;

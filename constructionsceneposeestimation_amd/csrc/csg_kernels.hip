@@ -1159,6 +1159,13 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
     return;
   }
   if (!(DBG(c.dbg) & 4u) && g2.y != kNoAlpha) {
+    if (DBG(c.dbg) & 512u) {   // profiling: wave executions of the alpha test and their active lanes
+      const uint64_t m = __ballot(1);
+      if ((uint32_t)__lane_id() == (uint32_t)__ffsll((unsigned long long)m) - 1u) {
+        atomicAdd(&c.ctr[12], 1u);
+        atomicAdd(&c.ctr[13], (uint32_t)__popcll(m));
+      }
+    }
     const bool pass = alpha_ok();
     if (DBG(c.dbg) & 512u) atomicAdd(&c.ctr[pass ? 6 : 5], 1u);   // profiling: alpha tests passed / failed
     if (!pass) return;
@@ -1345,6 +1352,13 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
       }
       __syncthreads();
       for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kBlock) {
+        if (DBG(b.dbg) & 512u) {   // profiling: level-2 wave iterations and their active lanes
+          const uint64_t m = __ballot(1);
+          if ((uint32_t)__lane_id() == (uint32_t)__ffsll((unsigned long long)m) - 1u) {
+            atomicAdd(&b.overflow[14], 1u);
+            atomicAdd(&b.overflow[15], (uint32_t)__popcll(m));
+          }
+        }
         const uint32_t w = L.starts[j >> 5], nb = L.before[j >> 5];
         const uint32_t rank = nb + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31u - (j & 31u))));
         const uint32_t spj = L.span[rank - 1u];
