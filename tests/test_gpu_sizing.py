@@ -177,3 +177,26 @@ def test_hinted_pools_chains_and_reordered_heavy_chain():
         assert np.array_equal(got["instance"], ref["instance"][heavy])
         wi = r.work_info()
         assert wi["hinted"] == 0 and wi["records_per_frame"] == info["records_per_frame"]
+
+
+def test_hinted_pools_c5_4k_every_output():
+    """C5 at 3840x2160 with every per-pixel output (depth, f16 normals, world
+    points, stats) through tight chain pools (margin 0, chains of 3 frames):
+    byte-identical to a context sized for every scene triangle."""
+    from constructionsceneposeestimation_amd.renderer import Renderer
+    from constructionsceneposeestimation_amd.workload import Workload
+    wl = Workload("C5", seed=3)
+    fids = [1, 7, 12, 18, 25, 29]
+    epochs, fr = _batch(wl, fids)
+    want = ("rgb", "instance", "depth", "normals", "points", "keypoints", "stats")
+    with Renderer(wl.scene, wl.width, wl.height, max_frames=len(fids), frames_per_launch=3) as full:
+        _upload(full, wl, epochs)
+        ref = full.render(fr, want=want)
+    with Renderer(wl.scene, wl.width, wl.height, max_frames=len(fids), frames_per_launch=3) as r:
+        _upload(r, wl, epochs)
+        info = r.size_work(fr, margin=0.0)
+        assert info["hinted"] == 1 and info["pool_records"] < 3 * info["records_per_frame"]
+        got = r.render(fr, want=want)
+        assert r.work_info()["hinted"] == 1          # no overflow: the hints held
+    for k in ref:
+        assert np.array_equal(np.asarray(got[k]).view(np.uint8), np.asarray(ref[k]).view(np.uint8)), k
