@@ -1,8 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark: annotated frames/s of the render + annotate hot path on MI355X.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
-N > 1 it is launched once per GPU by ``torch.distributed.run``.  One *step*
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  For
+N > 1 it runs one process per GPU: either launched once per GPU by
+``torch.distributed.run`` (RANK / WORLD_SIZE in the environment), or -- a
+plain ``python bench.py --gpus N`` -- this process starts the N ranks itself
+as fresh child processes before anything touches the GPU (``launch_ranks``),
+waits for all of them and forwards rank 0's line; if any rank fails it exits
+non-zero with no line.  One *step*
 = one batch of ``--frames-per-step`` frames of workload C3 (BASELINE.json
 configs[2]: world2 + rigged-human proxies, 1920x1080, RGB + instance
 segmentation + 2D keypoints) rendered into HBM-resident output buffers.
@@ -52,11 +57,11 @@ RECORD_BYTES = 80 + 4  # k_setup writes one 80-B raster record + its 4-B tile re
 # short kernels' fixed cost are paid once per launch (C3 frames/s with the work
 # buffers sized by csg_size_work: 960 -> 22.62k, 1,920 -> 22.80k, 2,880 ->
 # 22.90k, 3,840 -> 22.92k; profiles/r04/ab/frames_per_step.txt).  At 2,880 a
-# rank holds ~120 GB of work buffers and ~42 GB of outputs on its 288-GB GPU.
+# rank holds ~68 GB of work buffers and ~42 GB of outputs on its 288-GB GPU.
 DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 10, 2, 2880
 # Larger frames (C5 at 3840x2160 with depth, normals and points: ~240 MB of
 # outputs per frame) take 480 frames per step (240 -> 6.30k, 480 -> 6.34k
-# frames/s): ~115 GB of outputs and ~28 GB of work per rank.
+# frames/s): ~115 GB of outputs and ~16 GB of work per rank.
 LARGE_FRAME_PIXELS, LARGE_FRAMES_PER_STEP = 1920 * 1080, 480
 MAX_SETS = 65536   # transform sets per context (kMaxSets, csg_api.cpp)
 
@@ -119,19 +124,114 @@ def sum_over_ranks(vals: List[int], world: int) -> List[int]:
     return [int(v) for v in t.tolist()]
 
 
-def shard_report(timed: List[int], world: int) -> dict:
+def shard_report(timed: List[int], world: int, device: Optional[dict] = None) -> dict:
     """Each rank's timed frame ids gathered on every rank (gloo): the seed
-    shards must be disjoint, and their union is what ``value`` counts."""
-    lists = [list(timed)]
+    shards must be disjoint, and their union is what ``value`` counts.
+    ``device`` (this rank's GPU: ordinal, the process's device count, PCI
+    address) is gathered beside them, so a line proves N ranks on N distinct
+    devices -- or says that ranks shared one (a rehearsal on a smaller box)."""
+    lists = [(list(timed), device)]
     if world > 1:
         import torch.distributed as dist
         lists = [None] * world
-        dist.all_gather_object(lists, list(timed))
-    sets = [set(x) for x in lists]
+        dist.all_gather_object(lists, (list(timed), device))
+    sets = [set(x) for x, _ in lists]
     union = set().union(*sets)
-    return {"ranks": world, "timed_frames_per_rank": [len(x) for x in lists],
-            "union": len(union), "disjoint": len(union) == sum(len(x) for x in lists),
-            "epochs_mod_world": [sorted({(f // 10) % world for f in x}) for x in lists]}
+    rep = {"ranks": world, "timed_frames_per_rank": [len(x) for x, _ in lists],
+           "union": len(union), "disjoint": len(union) == sum(len(x) for x, _ in lists),
+           "epochs_mod_world": [sorted({(f // 10) % world for f in x}) for x, _ in lists]}
+    devs = [d for _, d in lists]
+    if all(d is not None for d in devs):
+        ids = [d.get("pci") or d["device"] for d in devs]
+        rep["devices"] = devs
+        rep["distinct_devices"] = len(set(ids))
+        rep["shared_devices"] = len(set(ids)) < world
+    return rep
+
+
+# ---------------------------------------------------------------------------
+# N ranks from a plain `python bench.py --gpus N` (no torchrun in front)
+# ---------------------------------------------------------------------------
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _die_with_parent():   # pragma: no cover - runs in the forked child before exec
+    try:
+        import ctypes
+        import signal
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)   # PR_SET_PDEATHSIG
+    except Exception:
+        pass
+
+
+def launch_ranks(n: int, child_argv: List[str], env: Optional[Dict[str, str]] = None,
+                 out=None, poll_s: float = 0.2, grace_s: float = 10.0) -> int:
+    """Start ``n`` fresh child processes running ``child_argv`` -- one rank
+    each, RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR 127.0.0.1 and a
+    free MASTER_PORT -- wait for all of them, and write rank 0's JSON line(s)
+    to ``out`` (stdout).  The children are started with ``subprocess`` (never
+    exec) from a process that has not touched the GPU; their stderr is
+    inherited, their stdout captured.  If any child fails, the others are
+    terminated (their own PIDs only), nothing is written and the return code
+    is non-zero (the first failure's, or 1)."""
+    import subprocess
+    import tempfile
+    out = out or sys.stdout
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", ROLE_RANK="0", ROLE_WORLD_SIZE=str(n))
+    procs, files = [], []
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r), ROLE_RANK=str(r))
+            fh = tempfile.TemporaryFile(mode="w+")
+            files.append(fh)
+            procs.append(subprocess.Popen(child_argv, env=e, stdout=fh, stderr=None, preexec_fn=_die_with_parent))
+        failed = 0
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                failed = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+        if failed:
+            log(f"bench: a rank failed (exit {failed}); stopping the other ranks, no result")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            t_end = time.time() + grace_s
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, t_end - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return failed if failed > 0 else 1
+        files[0].seek(0)
+        lines = [ln for ln in files[0].read().splitlines() if ln.startswith("{")]
+        if not lines:
+            log("bench: rank 0 printed no result line")
+            return 1
+        for ln in lines:
+            print(ln, file=out, flush=True)
+        return 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for fh in files:
+            fh.close()
 
 
 def median_time(fn: Callable[[], None], runs: int = 5, warmup: int = 1, what: str = "") -> float:
@@ -196,6 +296,16 @@ def cpu_model() -> str:
         pass
     import platform
     return platform.processor() or "unknown"
+
+
+def device_pci(ordinal: int) -> Optional[str]:
+    """PCI address of GPU ``ordinal`` (domain:bus:device), or None."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(ordinal)
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    except Exception:
+        return None
 
 
 def available_cpus() -> int:
@@ -293,6 +403,11 @@ def main():
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # a plain `python bench.py --gpus N`: start the N ranks here, before
+        # torch is imported (nothing in this process touches the GPU)
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -325,6 +440,8 @@ def main():
     local = local % ndev if ndev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    device_info = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": local,
+                   "device_count": ndev, "pci": device_pci(local)}
     K, W = args.steps, args.warmup
     wl = Workload(args.workload, seed=args.seed)
     H, Wd = wl.height, wl.width
@@ -539,7 +656,7 @@ def main():
             v_, p_, ref = ver.render(sample_frames, 2)
             bad = ver.compare(sample_frames, v_, p_, ref, gpu_sample)
     n_checked, n_bad = sum_over_ranks([len(sample_frames), len(bad)], world)
-    shards = shard_report(timed_frames(fids, W, K, F), world)
+    shards = shard_report(timed_frames(fids, W, K, F), world, device_info)
     if n_bad:
         for b in bad[:20]:
             log(f"[rank {rank}] VERIFY FAILED: {b}")

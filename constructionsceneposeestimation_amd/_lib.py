@@ -12,7 +12,7 @@ from typing import Optional
 PKG = os.path.dirname(os.path.abspath(__file__))
 # CSG_LIB names an alternative build of the same ABI (A/B timing of kernel variants)
 LIB_PATH = os.environ.get("CSG_LIB") or os.path.join(PKG, "libcsg.so")
-ABI_VERSION = 10  # CSG_ABI_VERSION in include/csg_api.h
+ABI_VERSION = 11  # CSG_ABI_VERSION in include/csg_api.h
 KEEP_TEXTURE = -2  # CSG_KEEP_TEXTURE
 COVERED_UNKNOWN = 0x80000000  # csg_outputs.label_covered flag: a tile held more than 32 labels
 ERR_CAPACITY = -6  # CSG_ERR_CAPACITY
@@ -93,7 +93,7 @@ class WorkInfo(C.Structure):
                 ("frames_per_launch", C.c_uint32), ("sized_frames", C.c_uint32), ("max_records", C.c_uint32),
                 ("max_bins", C.c_uint32), ("mean_records", C.c_double), ("mean_bins", C.c_double),
                 ("work_bytes", C.c_uint64), ("pool_records", C.c_uint64), ("pool_bins", C.c_uint64),
-                ("hinted", C.c_uint32), ("pad", C.c_uint32)]
+                ("hinted", C.c_uint32), ("hint_retries", C.c_uint32)]
 
 
 _lib: Optional[C.CDLL] = None

@@ -26,10 +26,16 @@ using namespace csg;
 
 namespace {
 
+// A device allocation owned by one object: freed by release() or at the end
+// of its scope (a local scratch buffer cannot leak on an early error return).
 template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   hipError_t alloc(size_t count) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipFree(p);
@@ -118,9 +124,10 @@ struct csg_ctx {
   uint32_t rec_cap = 0, bin_cap = 0, work_frames = 0;
   uint64_t rec_pool = 0, bin_pool = 0;            // pool entries allocated
   bool use_hints = false;                         // csg_size_work sized the pools from frame hints
+  uint32_t hint_fallbacks = 0;                    // re-renders the hinted pools caused (csg_work_info)
   uint64_t plan_rec_pool = 0, plan_bin_pool = 0;  // ... to these
   DevBuf<Slab> slab;                              // [chain frames] (k_plan)
-  DevBuf<uint64_t> plan_need;                     // [2] pool entries the last chain asked for
+  DevBuf<uint64_t> plan_need;                     // [2] pool entries the batch's largest chain asked for (k_plan)
   DevBuf<FrameDev> frames;
   // Pinned staging ring for host frame records: a batch's records are copied
   // into the next slot, and a slot is reused only after the H2D copy that read
@@ -284,8 +291,8 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   c->chain_frames = cfg->frames_per_launch ? cfg->frames_per_launch : kAutoChainFrames;
   if (const char* v = getenv("CSG_CHAIN")) c->chain_frames = (uint32_t)std::max(1, atoi(v));
   c->chain_frames = std::min(c->chain_frames, cfg->max_frames);
-  c->tiles_x = (cfg->width + kTile - 1) / kTile;
-  c->tiles_y = (cfg->height + kTile - 1) / kTile;
+  c->tiles_x = (cfg->width + kTileW - 1) / kTileW;
+  c->tiles_y = (cfg->height + kTileH - 1) / kTileH;
   c->n_tiles = c->tiles_x * c->tiles_y;
   hipError_t e = hipSetDevice(cfg->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -957,6 +964,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   // The batch runs as consecutive launch chains of `chain_frames` frames (by
   // default one chain); the work buffers hold one chain.
   const uint32_t G = c->chain_frames;
+  HIP_TRY(c, hipMemsetAsync(c->plan_need.p, 0, 2 * sizeof(uint64_t), st));   // k_plan: max over the chains
   for (uint32_t c0 = 0; c0 < F; c0 += G) {
     const uint32_t Fc = std::min(G, F - c0);
     BatchDev bc = b;
@@ -1157,12 +1165,31 @@ int csg_render_batch(csg_ctx* c, const csg_frame* frames, uint32_t n_frames, con
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (ov & (kOvBadSet | kOvBadKpSet))   // host frames are validated before launch: cannot happen
       return c->fail(CSG_ERR_DEVICE, "render: unexpected set error flags %u", ov);
-    // Pools planned from frame hints (csg_size_work) overflowed: stale hints
-    // (scene edits after sizing), unmeasured frames, or another grouping of
-    // frames into chains than the sizing assumed.  First retry: no hints, every
-    // frame at the per-frame caps (the largest measured counts with the margin).
+    // Pools planned from frame hints (csg_size_work) overflowed: another
+    // grouping of frames into chains than the sizing assumed (a chain's hints
+    // add up past the pool: k_plan's need[]), or stale hints / unmeasured
+    // frames (a frame past its own hint).  The first is retried with the pools
+    // grown to the largest chain's need, hints kept; the second without hints,
+    // every frame at the per-frame caps (the largest measured counts with the
+    // margin).  A later csg_size_work turns the hints back on.
     if (c->use_hints) {
+      uint64_t need[2] = {0, 0};
+      HIP_TRY(c, hipMemcpy(need, c->plan_need.p, sizeof(need), hipMemcpyDeviceToHost));
+      if (need[0] > c->rec_pool || need[1] > c->bin_pool) {
+        fprintf(stderr, "[csg] hinted work pools too small for this grouping of frames (records %llu > %llu or "
+                        "bin entries %llu > %llu): pools grown, re-rendering\n",
+                (unsigned long long)need[0], (unsigned long long)c->rec_pool, (unsigned long long)need[1],
+                (unsigned long long)c->bin_pool);
+        c->plan_rec_pool = std::max<uint64_t>(c->plan_rec_pool, need[0]);
+        c->plan_bin_pool = std::max<uint64_t>(c->plan_bin_pool, need[1]);
+        ++c->hint_fallbacks;
+        continue;
+      }
+      fprintf(stderr, "[csg] a frame overflowed its work hint (stale hints or an unmeasured frame): hints off, "
+                      "re-rendering at the per-frame caps (%u records, %u bin entries per frame); csg_size_work "
+                      "turns them back on\n", c->rec_cap, c->bin_cap);
       c->use_hints = false;
+      ++c->hint_fallbacks;
       continue;
     }
     // grow the overflowed capacity and re-render (results are a pure function
@@ -1404,6 +1431,7 @@ static void fill_work_info(const csg_ctx* c, csg_work_info* out) {
     out->pool_bins = (uint64_t)c->chain_frames * ((bin + 3u) & ~3u);
   }
   out->hinted = c->use_hints ? 1u : 0u;
+  out->hint_retries = c->hint_fallbacks;
   out->work_bytes = work_bytes_for(c, c->chain_frames, out->pool_records, out->pool_bins);
 }
 

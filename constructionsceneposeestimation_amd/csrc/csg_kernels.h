@@ -6,13 +6,31 @@
 
 namespace csg {
 
-constexpr int kTile = 32;                 // screen tile edge (pixels)
-constexpr int kTilePix = kTile * kTile;   // 1024 pixels, one 256-thread workgroup
+// Screen tiles: one k_raster workgroup each, 4 consecutive pixels of a tile
+// row per thread in the resolve.  32 x 32 (1,024 pixels, 256 threads) is the
+// production shape; CSG_TILE_W / CSG_TILE_H build the other shapes measured
+// against it (profiles/r05/ab/tile_shape.txt).
+#ifndef CSG_TILE_W
+#define CSG_TILE_W 32
+#endif
+#ifndef CSG_TILE_H
+#define CSG_TILE_H 32
+#endif
+constexpr int kTileW = CSG_TILE_W;           // tile width (pixels)
+constexpr int kTileH = CSG_TILE_H;           // tile height (pixels)
+constexpr int kTilePix = kTileW * kTileH;
+constexpr int kRasterBlock = kTilePix / 4;   // k_raster threads per workgroup
+static_assert((kTileW == 16 || kTileW == 32 || kTileW == 64) && (kTileH == 16 || kTileH == 32) &&
+                  kRasterBlock >= 64 && kRasterBlock <= 256,
+              "tile shapes: width 16/32/64, height 16/32, 64..256 threads");
 constexpr int kBlock = 256;
 constexpr uint32_t kUidShift = 20;        // spec: uid = (instance << 20) | triangle (tie order); see SceneDev::uid_shift
 constexpr uint32_t kMaxInstances = 1u << (32 - kUidShift);
 constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
-constexpr int kMaxLdsLabels = 256;        // per-label pixel stats kept in LDS
+#ifndef CSG_LDS_LABELS
+#define CSG_LDS_LABELS 256
+#endif
+constexpr int kMaxLdsLabels = CSG_LDS_LABELS;   // per-label pixel stats kept in LDS (the rest: global atomics)
 constexpr int kCovSlots = 32;             // labels per tile in k_raster's coverage table (occlusion)
 constexpr uint32_t kCovUnknown = 0x80000000u;   // covered[] flag: a tile held more than kCovSlots labels
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each
@@ -174,8 +192,9 @@ struct BatchDev {
 // launchers (all enqueue on `st`)
 // k_plan: each frame's slab from its hints (use_hints; 0 = none) or the
 // default caps, packed back to back; frames past a pool's end get what is
-// left (possibly nothing: they overflow).  need[0], need[1]: the pool
-// entries the chain asked for.  Pools are multiples of 4 entries.
+// left (possibly nothing: they overflow).  need[0], need[1]: raised to the
+// pool entries the chain asked for (a running maximum over the batch's
+// chains).  Pools are multiples of 4 entries.
 void launch_plan(const FrameDev* frames, uint32_t F, uint32_t def_rec, uint32_t def_bin, uint64_t rec_pool,
                  uint64_t bin_pool, int use_hints, Slab* slab, uint64_t* need, hipStream_t st);
 // csg_size_work's hint for a measured count: count x (1 + margin) + pad, 4-aligned, < 2^31

@@ -265,10 +265,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// exclusive scan over the 256-thread block; `wsum` is LDS[4].  kTrail = false
-// skips the closing barrier: for a `wsum` whose next scan is already ordered
-// after this one's reads by some other barrier.
-template <bool kTrail = true>
+// exclusive scan over an NB-thread block; `wsum` is LDS[NB / 64].  kTrail =
+// false skips the closing barrier: for a `wsum` whose next scan is already
+// ordered after this one's reads by some other barrier.
+template <bool kTrail = true, int NB = kBlock>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
   const uint32_t inc = wave_incl_scan(v);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -276,7 +276,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   __syncthreads();
   uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int k = 0; k < kBlock / 64; ++k) {
+  for (int k = 0; k < NB / 64; ++k) {
     const uint32_t x = wsum[k];
     off += (k < w) ? x : 0u;
     tot += x;
@@ -454,7 +454,7 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
 
 __device__ __forceinline__ uint32_t rec_tile_rect(const SubRec& r) {
   const uint32_t px0 = r.g1.z & 0xFFFFu, py0 = r.g1.z >> 16, px1 = r.g1.w & 0xFFFFu, py1 = r.g1.w >> 16;
-  return (px0 / kTile) | ((py0 / kTile) << 8) | ((px1 / kTile) << 16) | ((py1 / kTile) << 24);
+  return (px0 / kTileW) | ((py0 / kTileH) << 8) | ((px1 / kTileW) << 16) | ((py1 / kTileH) << 24);
 }
 
 __device__ __forceinline__ uint32_t rect_area(uint32_t rc) {
@@ -854,9 +854,11 @@ __global__ __launch_bounds__(64) void k_plan(const FrameDev* __restrict__ frames
     cr += __shfl(ir, 63, 64);
     cb += __shfl(ib, 63, 64);
   }
+  // the largest chain of the batch (chains run one after another on the
+  // stream; the host zeroes need[] before a batch and reads it on overflow)
   if (lane == 0) {
-    need[0] = cr;
-    need[1] = cb;
+    need[0] = max(need[0], cr);
+    need[1] = max(need[1], cb);
   }
 }
 
@@ -1032,8 +1034,13 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 #endif
 #define CSG_RASTER_ATTR \
   __attribute__((amdgpu_waves_per_eu(kCov ? CSG_COV_WAVES : CSG_WAVES, kCov ? CSG_COV_WAVES : CSG_WAVES)))
-constexpr int kStage = CSG_STAGE;     // records staged per raster batch (<= kBlock)
-static_assert(kStage <= kBlock && CSG_COV_STAGE <= kBlock, "one staged record per thread");
+constexpr int kStage = CSG_STAGE;     // records staged per raster batch (<= kRasterBlock)
+static_assert(kStage <= kRasterBlock && CSG_COV_STAGE <= kRasterBlock, "one staged record per thread");
+constexpr int kRB = kRasterBlock;
+// level-2 items of one level-1 round: up to kRB spans of up to kTileW pixels,
+// as 32-item words of the start bitmap
+constexpr int kL2Words = kRB * kTileW / 32;
+constexpr int kColWords = (kTileW + 31) / 32;   // 32-bit column masks per tile row (label statistics)
 template <bool kCov>
 constexpr int kStageOf = kCov ? CSG_COV_STAGE : kStage;
 template <int NS>
@@ -1044,12 +1051,12 @@ struct RecImage {
 // Coverage table of k_raster<true> (occlusion, GDP:1780-1790 occlusionRatio):
 // for each label seen in the tile, the pixels some fragment of it covers
 // (covered centre, depth in range, alpha test passed; no depth test), as a
-// 32x32 bit image.  A label that finds no slot (more than kCovSlots labels in
+// bit image of the tile (bit p & 31 of word p >> 5, p = ly * kTileW + lx).  A label that finds no slot (more than kCovSlots labels in
 // one tile) marks the tile: its labels are then flagged unknown and their
 // counts are not added, so the result does not depend on fragment order.
 struct CovLds {
   uint32_t keys[kCovSlots];             // label of each slot (kNoAlpha: empty)
-  uint32_t mask[kCovSlots][kTile];      // per slot: bit lx of word ly
+  uint32_t mask[kCovSlots][kTilePix / 32];   // per slot: the tile's pixels as bits
   uint32_t ovf;                         // some label found no slot
 };
 
@@ -1076,7 +1083,8 @@ __device__ __forceinline__ void cov_mark(const RasterCtx& c, uint32_t label, int
     uint32_t cur = t.keys[idx];
     if (cur == kNoAlpha) cur = atomicCAS(&t.keys[idx], kNoAlpha, label);
     if (cur == kNoAlpha || cur == label) {
-      atomicOr(&t.mask[idx][ly], 1u << lx);
+      const uint32_t px = (uint32_t)(ly * kTileW + lx);
+      atomicOr(&t.mask[idx][px >> 5], 1u << (px & 31u));
       return;
     }
   }
@@ -1125,7 +1133,7 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
     return alpha_pass(c.aquad, c.acls, (g2.y & 0xFFFFFFu) * kTexAlign, g4.w, (int)(g2.y >> 24), uv.x, uv.y);
   };
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
-  unsigned long long* z = &c.zb[ly * kTile + lx];
+  unsigned long long* z = &c.zb[ly * kTileW + lx];
   if constexpr (kCov) {
     // A fragment has two possible effects: its label's coverage bit and the
     // depth minimum.  One that loses early-z and whose bit is already set has
@@ -1137,12 +1145,16 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
     bool mark = false;
     if (lab >= 0) {
       slot = cov_find(c, (uint32_t)lab);
-      mark = slot < 0 || !((c.cov->mask[slot][ly] >> lx) & 1u);
+      const uint32_t px = (uint32_t)(ly * kTileW + lx);
+      mark = slot < 0 || !((c.cov->mask[slot][px >> 5] >> (px & 31u)) & 1u);
     }
     if (!zwin && !mark) return;
     if (g2.y != kNoAlpha && !alpha_ok()) return;
     if (mark) {
-      if (slot >= 0) atomicOr(&c.cov->mask[slot][ly], 1u << lx);
+      if (slot >= 0) {
+        const uint32_t px = (uint32_t)(ly * kTileW + lx);
+        atomicOr(&c.cov->mask[slot][px >> 5], 1u << (px & 31u));
+      }
       else cov_mark(c, (uint32_t)lab, lx, ly);
     }
     if (zwin) atomicMin(z, key);
@@ -1188,8 +1200,8 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 #pragma unroll
   for (int k = 0; k < kRecGroups; ++k) img.q[k][slot] = q[k];
   const uint32_t p0 = q[1].z, p1 = q[1].w;            // px0 | py0 << 16, px1 | py1 << 16
-  int y0 = max((int)(p0 >> 16), oy), y1 = min((int)(p1 >> 16), oy + kTile - 1);
-  const int x0 = max((int)(p0 & 0xFFFFu), ox), x1 = min((int)(p1 & 0xFFFFu), ox + kTile - 1);
+  int y0 = max((int)(p0 >> 16), oy), y1 = min((int)(p1 >> 16), oy + kTileH - 1);
+  const int x0 = max((int)(p0 & 0xFFFFu), ox), x1 = min((int)(p1 & 0xFFFFu), ox + kTileW - 1);
   if (x0 > x1 || y0 > y1) return 0u;
   // Rows of the triangle inside this tile's column strip: the y-range of the
   // triangle clipped to the pixel-centre lines x0..x1, in float relative to
@@ -1245,11 +1257,11 @@ struct RasterLds {
   uint16_t before1[NS + 1];             // records starting before item 32*d
   uint32_t crec[NS];                    // compact record: slot | first item << 8
   uint8_t row0[NS];                     // first tile row of each staged record | 0x80 if small
-  uint32_t span[kBlock];                // rec | ly << 8 | (ex2 - xl + 32) << 16
-  uint32_t starts[kBlock];              // bit i: a span starts at level-2 item i (<= 256 spans x 32 px)
-  uint16_t before[kBlock + 1];          // spans starting before item 32*d
-  uint32_t wsum[kBlock / 64];           // the batch scan's wave totals
-  uint32_t wsum2[kBlock / 64];          // the level-2 scan's (each reused only after other barriers)
+  uint32_t span[kRB];                   // rec | ly << 8 | (ex2 - xl + kTileW) << 16
+  uint32_t starts[kL2Words];            // bit i: a span starts at level-2 item i (<= kRB spans x kTileW px)
+  uint16_t before[kL2Words + 1];        // spans starting before item 32*d
+  uint32_t wsum[kRB / 64];              // the batch scan's wave totals
+  uint32_t wsum2[kRB / 64];             // the level-2 scan's (each reused only after other barriers)
 };
 
 // Block-level two-level expansion of kStage-record batches.
@@ -1291,7 +1303,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
     if (tid < NS) L.starts1[tid] = 0u;   // ordered before the atomics by the scan's barriers
     if (tid == 0) L.before1[0] = 0;
     uint32_t tot1p;
-    const uint32_t ex1p = block_excl_scan<false>(rows | (rows ? 0x10000u : 0u), L.wsum, tot1p);
+    const uint32_t ex1p = block_excl_scan<false, kRB>(rows | (rows ? 0x10000u : 0u), L.wsum, tot1p);
     const uint32_t tot1 = tot1p & 0xFFFFu;
     if (rows) {
       const uint32_t ex1 = ex1p & 0xFFFFu, ci = ex1p >> 16, e_end = ex1 + rows;
@@ -1300,7 +1312,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
       if ((e_end & ~31u) > ex1) L.before1[e_end >> 5] = (uint16_t)(ci + 1u);
     }
     __syncthreads();
-    for (uint32_t c1 = 0; c1 < ((DBG(b.dbg) & 256u) ? 0u : tot1); c1 += kBlock) {
+    for (uint32_t c1 = 0; c1 < ((DBG(b.dbg) & 256u) ? 0u : tot1); c1 += kRB) {
       const uint32_t j1 = c1 + tid;
       uint32_t w2 = 0, sp = 0;
       int xl = 0;
@@ -1312,7 +1324,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
         const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
         const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
         const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
-        const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTile - 1);
+        const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTileW - 1);
         const uint32_t r0b = L.row0[k];
         const int ly = (int)(r0b & 31u) + (int)(j1 - first);
         int xr;
@@ -1339,19 +1351,31 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
       // span starts plus, per 32-item word, the spans starting before it (the
       // one span crossing each word boundary writes it) -- two independent
       // LDS reads and a popcount instead of a 4-step search.
-      L.starts[tid] = 0u;                 // ordered before the atomics by the scan's barriers
+      // zeroed before the atomics below (ordered by the scan's barriers)
+      if constexpr (kL2Words >= kRB) {
+#pragma unroll
+        for (int w = 0; w < kL2Words / kRB; ++w) L.starts[tid + w * kRB] = 0u;
+      } else if (tid < kL2Words) {
+        L.starts[tid] = 0u;
+      }
       if (tid == 0) L.before[0] = 0;
       uint32_t totp;
-      const uint32_t exp = block_excl_scan<false>(w2 | (w2 ? 0x10000u : 0u), L.wsum2, totp);
+      const uint32_t exp = block_excl_scan<false, kRB>(w2 | (w2 ? 0x10000u : 0u), L.wsum2, totp);
       const uint32_t ex2 = exp & 0xFFFFu, tot2 = totp & 0xFFFFu;
       if (w2) {
         const uint32_t ci = exp >> 16, e_end = ex2 + w2;
-        L.span[ci] = sp | ((ex2 - (uint32_t)xl + 32u) << 16);
+        L.span[ci] = sp | ((ex2 - (uint32_t)xl + (uint32_t)kTileW) << 16);
         atomicOr(&L.starts[ex2 >> 5], 1u << (ex2 & 31u));
-        if ((e_end & ~31u) > ex2) L.before[e_end >> 5] = (uint16_t)(ci + 1u);   // word boundary inside
+        // the spans starting before each 32-item word boundary inside (ex2, e_end]
+        // (a span of <= 32 items crosses at most one)
+        if constexpr (kTileW <= 32) {
+          if ((e_end & ~31u) > ex2) L.before[e_end >> 5] = (uint16_t)(ci + 1u);
+        } else {
+          for (uint32_t d = (ex2 >> 5) + 1u; d <= (e_end >> 5); ++d) L.before[d] = (uint16_t)(ci + 1u);
+        }
       }
       __syncthreads();
-      for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kBlock) {
+      for (uint32_t j = tid; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += kRB) {
         if (DBG(b.dbg) & 512u) {   // profiling: level-2 wave iterations and their active lanes
           const uint64_t m = __ballot(1);
           if ((uint32_t)__lane_id() == (uint32_t)__ffsll((unsigned long long)m) - 1u) {
@@ -1362,7 +1386,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
         const uint32_t w = L.starts[j >> 5], nb = L.before[j >> 5];
         const uint32_t rank = nb + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31u - (j & 31u))));
         const uint32_t spj = L.span[rank - 1u];
-        fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + 32u - (spj >> 16)), (int)((spj >> 8) & 255u));
+        fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + (uint32_t)kTileW - (spj >> 16)), (int)((spj >> 8) & 255u));
       }
       __syncthreads();
     }
@@ -1523,21 +1547,25 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
 #ifndef CSG_SHADE_SLOTS
 #define CSG_SHADE_SLOTS 116
 #endif
-constexpr uint32_t kShadeSlots = CSG_SHADE_SLOTS;   // <= kBlock (one setup thread per slot)
-static_assert(kShadeSlots <= (uint32_t)kBlock && kShadeSlots < 255u, "one setup thread per slot; 8-bit slot ids");
+constexpr uint32_t kShadeSlots = CSG_SHADE_SLOTS;   // <= kRasterBlock (one setup thread per slot)
+static_assert(kShadeSlots <= (uint32_t)kRasterBlock && kShadeSlots < 255u, "one setup thread per slot; 8-bit slot ids");
 constexpr int kShadeProbes = 16;
 struct ResolveLds {
   uint32_t keys[kShadeSlots];       // uid or kNoAlpha (empty)
   uint32_t more;                    // a pixel is left for another round
   ShadeEntry tab[kShadeSlots];
-  uint32_t lstat[3][kMaxLdsLabels]; // per label: pixel count, column mask, row mask (tile-relative bits)
+  uint32_t lstat[2 + kColWords][kMaxLdsLabels];   // per label: pixel count, row mask, column mask(s) (tile-relative bits)
 };
 
 // The resolve's LDS aliases the raster loop's in a union inside k_raster.
-// (Measured: 31,776 B per workgroup keeps 5 per CU, 32,512 B gave 4;
-// 26,656 B keeps 6; 22,448 B keeps 7.)
+// (Measured with 4-wave workgroups: 31,776 B per workgroup keeps 5 per CU,
+// 32,512 B gave 4; 26,656 B keeps 6; 22,448 B keeps 7.)  Other workgroup
+// sizes (tile shapes): the same 160 KiB per CU less the 4-wave table's
+// observed slack, shared by waves * 4 / (waves per workgroup) workgroups.
 constexpr size_t lds_budget(int waves) {
-  return waves >= 8 ? 20480u : waves == 7 ? 22528u : waves == 6 ? 26700u : waves == 5 ? 32256u : 40960u;
+  return kRasterBlock == 256
+             ? (waves >= 8 ? 20480u : waves == 7 ? 22528u : waves == 6 ? 26700u : waves == 5 ? 32256u : 40960u)
+             : ((157696u / (size_t)(waves * 4 / (kRasterBlock / 64))) & ~511u);
 }
 static_assert((sizeof(RasterLds<kStage>) > sizeof(ResolveLds) ? sizeof(RasterLds<kStage>) : sizeof(ResolveLds)) +
                       kTilePix * 8 <= lds_budget(CSG_WAVES),
@@ -1611,15 +1639,15 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
                                            int oy) {
   const int tid = threadIdx.x;
   if (b.n_kp && ((b.kp_tiles[(size_t)f * b.tile_words + (tile >> 5)] >> (tile & 31u)) & 1u)) {
-    for (uint32_t k = tid; k < b.n_kp; k += kBlock) {
+    for (uint32_t k = tid; k < b.n_kp; k += kRB) {
       const size_t o = (size_t)f * b.n_kp + k;
       const uint32_t pp = b.kp_pix[o];
       const int px = (int)(pp & 0xFFFFu) - ox, py = (int)(pp >> 16) - oy;
-      if (pp == 0xFFFFFFFFu || px < 0 || px >= kTile || py < 0 || py >= kTile) continue;
+      if (pp == 0xFFFFFFFFu || px < 0 || px >= kTileW || py < 0 || py >= kTileH) continue;
       b.kp_vis[o] = (b.kp_w[o] <= INFINITY) ? 2 : 1;
     }
   }
-  const int ly = tid >> 3, lx0 = (tid & 7) * 4;
+  const int ly = tid / (kTileW / 4), lx0 = (tid % (kTileW / 4)) * 4;
   const int py = oy + ly, px0 = ox + lx0;
   if (py >= (int)s.H) return;
   const size_t o = (size_t)f * s.W * s.H + (size_t)py * s.W + px0;
@@ -1657,8 +1685,8 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
 // (4.1 KiB) is paid for with smaller batches (CSG_COV_STAGE records), so it
 // keeps 7 workgroups per CU.
 template <bool kCov>
-__global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, BatchDev b) {
-  __shared__ unsigned long long zb[kTilePix];        // 8 KiB (depth,uid) keys
+__global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDev s, BatchDev b) {
+  __shared__ unsigned long long zb[kTilePix];        // (depth,uid) keys: 8 KiB at 32 x 32
   constexpr int NS = kStageOf<kCov>;
   __shared__ union Lds {
     RasterSide<kCov> ra;                             // raster loop
@@ -1668,7 +1696,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   uint32_t tile;
   if (!swizzled_tile(blockIdx.x, s.tiles_x, s.tiles_y, tile)) return;
   const uint32_t f = blockIdx.y;
-  const int ox = (int)(tile % s.tiles_x) * kTile, oy = (int)(tile / s.tiles_x) * kTile;
+  const int ox = (int)(tile % s.tiles_x) * kTileW, oy = (int)(tile / s.tiles_x) * kTileH;
   const uint32_t* toff = b.tile_off + (size_t)f * (s.n_tiles + 1);
   const Slab sb = b.slab[f];
   const uint32_t beg = min(toff[tile], sb.bin_cap);
@@ -1677,14 +1705,14 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     empty_tile(s, b, f, tile, ox, oy);
     return;
   }
-  for (int p = tid; p < kTilePix; p += kBlock) zb[p] = kEmptyKey;
+  for (int p = tid; p < kTilePix; p += kRB) zb[p] = kEmptyKey;
   CovLds* covp = nullptr;
   int32_t* rlabel = nullptr;
   if constexpr (kCov) {
     covp = &L.ra.cov;
     rlabel = L.ra.rlabel;
     CovLds& covl = *covp;
-    for (int p = tid; p < kCovSlots * kTile; p += kBlock) (&covl.mask[0][0])[p] = 0u;
+    for (int p = tid; p < kCovSlots * (kTilePix / 32); p += kRB) (&covl.mask[0][0])[p] = 0u;
     if (tid < kCovSlots) covl.keys[tid] = kNoAlpha;
     if (tid == 0) covl.ovf = 0u;
   }
@@ -1696,19 +1724,20 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   raster_block<kCov, NS>(c, s, b, L.ra.r, beg, end, bins, recs, sb.rec_cap);
   __syncthreads();
   if constexpr (kCov) {
-    // per slot: popcount of its 32 mask words, 8 threads per slot (4 words
-    // each, lanes t..t+7 of one wave); the table is read-only from here on
+    // per slot: popcount of its kTilePix / 32 mask words, kTPS threads per
+    // slot (4 words each, consecutive lanes of one wave); the table is
+    // read-only from here on
     const CovLds& covl = *covp;
-    static_assert(kCovSlots * 8 == kBlock && kTile == 32, "8 threads x 4 words per slot");
-    const uint32_t sl = (uint32_t)tid >> 3, w0 = ((uint32_t)tid & 7u) * 4u;
+    constexpr int kTPS = kRB / kCovSlots;
+    static_assert(kTPS * 4 * 32 == kTilePix && kTPS <= 64, "4 words per thread, a slot's threads in one wave");
+    const uint32_t sl = (uint32_t)tid / kTPS, w0 = ((uint32_t)tid % kTPS) * 4u;
     uint32_t n = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) n += (uint32_t)__popc(covl.mask[sl][w0 + w]);
-    n += (uint32_t)__shfl_xor((int)n, 1, 64);
-    n += (uint32_t)__shfl_xor((int)n, 2, 64);
-    n += (uint32_t)__shfl_xor((int)n, 4, 64);
+#pragma unroll
+    for (int o = 1; o < kTPS; o <<= 1) n += (uint32_t)__shfl_xor((int)n, o, 64);
     const uint32_t lab = covl.keys[sl];
-    if ((tid & 7) == 0 && lab != kNoAlpha) {
+    if ((tid % kTPS) == 0 && lab != kNoAlpha) {
       if (covl.ovf) atomicOr(&c.gcov[lab], kCovUnknown);
       else atomicAdd(&c.gcov[lab], n);
     }
@@ -1722,12 +1751,12 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   // keypoint visibility against the finished z-buffer: W <= depth -> 2, else 1
   // (depth = 1/invW of the winning key, the value the resolve writes)
   if (b.n_kp && ((b.kp_tiles[(size_t)f * b.tile_words + (tile >> 5)] >> (tile & 31u)) & 1u)) {
-    for (uint32_t k = tid; k < b.n_kp; k += kBlock) {
+    for (uint32_t k = tid; k < b.n_kp; k += kRB) {
       const size_t o = (size_t)f * b.n_kp + k;
       const uint32_t pp = b.kp_pix[o];
       const int px = (int)(pp & 0xFFFFu) - ox, py = (int)(pp >> 16) - oy;
-      if (pp == 0xFFFFFFFFu || px < 0 || px >= kTile || py < 0 || py >= kTile) continue;
-      const unsigned long long key = zb[py * kTile + px];
+      if (pp == 0xFFFFFFFFu || px < 0 || px >= kTileW || py < 0 || py >= kTileH) continue;
+      const unsigned long long key = zb[py * kTileW + px];
       const float d = key == kEmptyKey ? INFINITY : rcp_ieee(__uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32)));
       b.kp_vis[o] = (b.kp_w[o] <= d) ? 2 : 1;
     }
@@ -1743,9 +1772,10 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   // asked for them (csg_outputs.inst_stats): otherwise no LDS table, no runs.
   const bool want_stats = b.stats != nullptr;
   const uint32_t nl = want_stats ? min(b.n_labels, (uint32_t)kMaxLdsLabels) : 0u;
-  uint32_t (*lstat)[kMaxLdsLabels] = L.q.lstat;
-  for (uint32_t l = tid; l < nl; l += kBlock) {
-    lstat[0][l] = 0; lstat[1][l] = 0; lstat[2][l] = 0;
+  uint32_t (*lstat)[kMaxLdsLabels] = L.q.lstat;   // [0] count, [1] row mask, [2..] column masks
+  for (uint32_t l = tid; l < nl; l += kRB) {
+#pragma unroll
+    for (int w = 0; w < 2 + kColWords; ++w) lstat[w][l] = 0;
   }
   // ---- resolve: 4 consecutive pixels per thread, one tile row per 8 threads.
   // Rounds: the tile's distinct winning triangles go into the shade table
@@ -1755,18 +1785,18 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   // A shaded pixel's z-buffer word is dead, so it takes the pixel's result
   // (rgb | id << 32) until the vector stores at the end: between phases a
   // thread keeps only bit masks and slot numbers in registers.
-  const int ly = tid >> 3, lx0 = (tid & 7) * 4;
+  const int ly = tid / (kTileW / 4), lx0 = (tid % (kTileW / 4)) * 4;
   const int py = oy + ly;
   const bool row_ok = py < (int)s.H;
   const int px0 = ox + lx0;
-  unsigned long long* zrow = &zb[ly * kTile + lx0];
+  unsigned long long* zrow = &zb[ly * kTileW + lx0];
   uint32_t pend = 0;                 // bit k: pixel k still to shade
   uint32_t inmask = 0;               // bit k: pixel k lies inside the frame
   // The depth visualisation's range (b.drange), from the winning keys: the
   // written depth is 1/invW (IEEE, monotone), so the tile's smallest depth is
   // 1/(largest invW), i.e. comes from the smallest key.  Reduced per wave here;
   // thread 0 combines the waves after the first round's barrier.
-  __shared__ uint32_t drw[2][kBlock / 64];
+  __shared__ uint32_t drw[2][kRB / 64];
   {
     const uint32_t sky = b.lights[b.fset[f]].sky & 0xFFFFFFu;
     const unsigned long long bgword = (unsigned long long)sky | (0xFFFFFFFFull << 32);   // id -1
@@ -1812,7 +1842,7 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
     if (first && b.drange && tid == 0) {   // the tile's depth range (see drw)
       uint32_t kmn = drw[0][0], kmx = drw[1][0];
 #pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) { kmn = min(kmn, drw[0][w]); kmx = max(kmx, drw[1][w]); }
+      for (int w = 1; w < kRB / 64; ++w) { kmn = min(kmn, drw[0][w]); kmx = max(kmx, drw[1][w]); }
       if (kmn <= kmx) {   // some pixel has a surface: depths 1/invW, valid (finite, > 0) by the depth range test
         const float dmin = rcp_ieee(__uint_as_float(0xFFFFFFFFu - kmn));
         const float dmax = rcp_ieee(__uint_as_float(0xFFFFFFFFu - kmx));
@@ -1870,9 +1900,11 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
         if (run >= 0 && (uint32_t)run < nl) {
           // the box as bit masks of the tile's columns and rows: 3 atomics per
           // run instead of 5 (min/max are the lowest and highest bits)
+          // (a run lies inside one thread's 4 pixels: one column word)
+          const uint32_t col = xmin - (uint32_t)ox;
           atomicAdd(&lstat[0][run], cnt);
-          atomicOr(&lstat[1][run], (0xFu >> (3u - (xmax - xmin))) << (xmin - (uint32_t)ox));
-          atomicOr(&lstat[2][run], 1u << ((uint32_t)qy - (uint32_t)oy));
+          atomicOr(&lstat[2 + (kColWords > 1 ? col >> 5 : 0u)][run], (0xFu >> (3u - (xmax - xmin))) << (col & 31u));
+          atomicOr(&lstat[1][run], 1u << ((uint32_t)qy - (uint32_t)oy));
         } else if (run >= 0 && b.stats && (uint32_t)run < b.n_labels) {   // beyond the LDS table
           uint32_t* st = b.stats + ((size_t)f * b.n_labels + (uint32_t)run) * 5;
           atomicAdd(&st[0], cnt);
@@ -1966,14 +1998,22 @@ __global__ __launch_bounds__(256) CSG_RASTER_ATTR void k_raster(SceneDev s, Batc
   if (b.stats) {
     __syncthreads();
     uint32_t* st = b.stats + (size_t)f * b.n_labels * 5;
-    for (uint32_t l = tid; l < nl; l += kBlock) {
+    for (uint32_t l = tid; l < nl; l += kRB) {
       const uint32_t cnt = lstat[0][l];
       if (cnt) {
-        const uint32_t cm = lstat[1][l], rm = lstat[2][l];
+        const uint32_t rm = lstat[1][l];
+        uint32_t cm = lstat[2][l], cm_hi = cm, lo_w = 0, hi_w = 0;   // column words: first / last non-empty
+#pragma unroll
+        for (int w = 1; w < kColWords; ++w) {
+          const uint32_t m = lstat[2 + w][l];
+          if (!cm && m) { cm = m; lo_w = (uint32_t)w; }
+          if (m) { cm_hi = m; hi_w = (uint32_t)w; }
+        }
+        if (!cm_hi) cm_hi = cm;
         atomicAdd(&st[l * 5 + 0], cnt);
-        atomicMin(&st[l * 5 + 1], (uint32_t)ox + (uint32_t)(__ffs(cm) - 1));
+        atomicMin(&st[l * 5 + 1], (uint32_t)ox + 32u * lo_w + (uint32_t)(__ffs(cm) - 1));
         atomicMin(&st[l * 5 + 2], (uint32_t)oy + (uint32_t)(__ffs(rm) - 1));
-        atomicMax(&st[l * 5 + 3], (uint32_t)ox + 31u - (uint32_t)__clz(cm));
+        atomicMax(&st[l * 5 + 3], (uint32_t)ox + 32u * hi_w + 31u - (uint32_t)__clz(cm_hi));
         atomicMax(&st[l * 5 + 4], (uint32_t)oy + 31u - (uint32_t)__clz(rm));
       }
     }
@@ -2037,7 +2077,7 @@ __global__ __launch_bounds__(256) void k_keypoints(SceneDev s, BatchDev b) {
   b.kp_pix[o] = vis ? ((uint32_t)px | ((uint32_t)py << 16)) : 0xFFFFFFFFu;
   b.kp_w[o] = dot4(pv + 8, p[0], p[1], p[2]);
   if (vis) {
-    const uint32_t t = (uint32_t)(py / kTile) * s.tiles_x + (uint32_t)(px / kTile);
+    const uint32_t t = (uint32_t)(py / kTileH) * s.tiles_x + (uint32_t)(px / kTileW);
     atomicOr(&b.kp_tiles[(size_t)f * b.tile_words + (t >> 5)], 1u << (t & 31u));
   }
 }
@@ -2209,8 +2249,8 @@ void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
   const uint32_t squares = ((s.tiles_x + kSq - 1) / kSq) * ((s.tiles_y + kSq - 1) / kSq);
   dim3 g(8 * kSq * kSq * ((squares + 7) / 8), F);
-  if (b.covered) hipLaunchKernelGGL(k_raster<true>, g, dim3(kBlock), 0, st, s, b);
-  else hipLaunchKernelGGL(k_raster<false>, g, dim3(kBlock), 0, st, s, b);
+  if (b.covered) hipLaunchKernelGGL(k_raster<true>, g, dim3(kRasterBlock), 0, st, s, b);
+  else hipLaunchKernelGGL(k_raster<false>, g, dim3(kRasterBlock), 0, st, s, b);
 }
 
 void launch_init_stats(const BatchDev& b, uint32_t F, hipStream_t st) {

@@ -123,7 +123,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
              resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
              writer_mode: str = "thread", renderers: int = 0, object_list: str = "visible",
-             occlusion: bool = False) -> dict:
+             occlusion: bool = False, sink: str = "disk") -> dict:
     """Render ``frames`` on one GPU and write them (``outputs``, default the
     reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
     add the depth .npy, the depth .npy + CSV, the point cloud, the normals).
@@ -139,7 +139,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     occlusionRatio) to the label files.  The reference never reads that field
     and its label schema (GDP:2056-2064) has none, so it is off by default: it
     needs the per-label unoccluded coverage, i.e. k_raster<true> (about +36%
-    raster time)."""
+    raster time).
+    ``sink`` "discard" runs the whole pipeline (render, GPU encode, copy
+    into the page-locked ring, writer threads) but writes every file to
+    /dev/null: the generator's steady-state rate without a file system."""
     if object_list not in OBJECT_LISTS:
         raise ValueError(f"object_list {object_list!r}: choose from {OBJECT_LISTS}")
     outs = set(REFERENCE_OUTPUTS if outputs is None else outputs)
@@ -174,7 +177,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     n_rend = renderers or (2 if gpu_files else 1)
     # the writer processes start here, before this process touches the GPU
     pool = WriterPool(output_spec(batch, wl.height, wl.width, wl.n_keypoints(), scene_labels(wl.scene), want),
-                      n_writers, n_slots=2 + n_rend, mode=writer_mode)
+                      n_writers, n_slots=2 + n_rend, mode=writer_mode, sink=sink)
     rends = [Renderer(wl.scene, wl.width, wl.height, max_frames=batch, device=device) for _ in range(n_rend)]
     r = rends[0]
     if gpu_files:   # page-locked slots, and buffers for the encoded files (an estimate, grown on demand)
@@ -193,6 +196,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         return out["label_covered"][k] if "label_covered" in out else None
 
     t_render = t_slot_wait = t_prep = t_main_wait = t_labels = 0.0
+    d2h = []   # bytes each batch copied to the host (files + arrays), appended by the render threads
     t0 = time.time()
     starts = list(range(0, len(frames), batch))
 
@@ -217,6 +221,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         slot = b % pool.n_slots
         r = rends[b % n_rend]
         tw = time.time()
+        if kinds:   # files buffers this renderer replaced at an earlier batch (grow_files)
+            pool.release_retired(r.free_host_buffer)
         arrays = pool.arrays(slot)          # (waits until the writers are done with the slot)
         tp = time.time()
         epochs = sorted({f // 10 for f in fb})
@@ -239,8 +245,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 offsets = r.copy_files(pool.grow_files(slot, need + need // 4, alloc=r.host_buffer,
                                                        free=r.free_host_buffer), len(fb) * nk)
             arrays["file_offsets"] = offsets
+            d2h.append(int(offsets[-1]) + sum(v.nbytes for v in out.values()))
         else:
             out = r.render(fr, want=want, out={k: v[:len(fb)] for k, v in arrays.items()})
+            d2h.append(sum(v.nbytes for v in out.values()))
         te = time.time()
         return fb, slot, out, (te - tr, tp - tw, tr - tp)
 
@@ -342,6 +350,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                              "frames_per_s": round(len(frames) / wall, 2) if wall > 0 else None,
                              "writers": n_writers, "writer_mode": writer_mode, "renderers": n_rend,
                              "writer_task_s": round(pool.task_s, 3), "teardown_s": round(t_teardown, 3),
+                             "d2h_bytes": int(sum(d2h)), "d2h_bytes_per_frame": round(sum(d2h) / max(len(frames), 1)),
+                             "d2h_gbs": round(sum(d2h) / wall / 1e9, 2) if wall > 0 else None,
+                             "render_busy": round(t_render / (wall * n_rend), 3) if wall > 0 else None,
+                             "sink": sink,
                              "writer_busy": round(pool.task_s / (wall * n_writers), 3) if wall > 0 else None,
                              "outputs": sorted(outs)}
     return summary
@@ -375,13 +387,15 @@ def main(argv=None):
                     help="add occlusion_ratio per object to the label files (not in the reference's schema; "
                          "costs the unoccluded-coverage raster)")
     ap.add_argument("--no-resume", action="store_true")
+    ap.add_argument("--sink", default="disk", choices=("disk", "discard"),
+                    help="discard: the whole pipeline, every file written to /dev/null (steady-state measurement)")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
                        a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
                        outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode, renderers=a.renderers,
-                       object_list=a.object_list, occlusion=a.occlusion)
+                       object_list=a.object_list, occlusion=a.occlusion, sink=a.sink)
     print(json.dumps(summary))
 
 

@@ -34,9 +34,17 @@ import numpy as np
 Layout = Dict[str, Tuple[int, tuple, str]]     # name -> (byte offset in a slot, shape, dtype)
 
 
-def _atomic(path: str, fn, *args) -> None:
+SINKS = ("disk", "discard")
+
+
+def _atomic(path: str, fn, *args, sink: str = "disk") -> None:
     """Write through ``path + '.tmp'`` and rename: a crash never leaves a
-    truncated file under the final name."""
+    truncated file under the final name.  Sink "discard" writes the same
+    bytes to /dev/null instead (the whole pipeline but the file system: a
+    steady-state measurement of render, encode, copy and writer threads)."""
+    if sink == "discard":
+        fn(os.devnull, *args)
+        return
     tmp = path + ".tmp"
     fn(tmp, *args)
     os.replace(tmp, path)
@@ -65,14 +73,14 @@ POINTCLOUD_HEADER = b"x y z r g b\n"   # the TXT's first line (np.savetxt header
 
 
 def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, str, Tuple[str, ...]]],
-                label: dict, label_path: str) -> Optional[dict]:
+                label: dict, label_path: str, sink: str = "disk") -> Optional[dict]:
     """Every file of frame ``k`` of a batch, then its label JSON (the resume
     marker, GDP:1357-1367 scans labels/).  ``files`` = (path, kind, array
     names); kind "encoded" names the file index j in the batch's files
     encoded on the GPU (arrays "files" + "file_offsets"); ``label`` is the
     label dict, or a callable that writes the label file to the path it is
     given (writers.LabelWriter); returns the frame's depth counts for the
-    quality log."""
+    quality log.  ``sink`` "discard": every file goes to /dev/null."""
     from . import writers as fileio
     from .labels import label_json_bytes
     for path, kind, keys in files:
@@ -85,25 +93,25 @@ def write_frame(arrays: Dict[str, np.ndarray], k: int, files: List[Tuple[str, st
             # GDP:723-725; the depth fallback saves only len(xyzrgb) > 0, :1755)
             if kind == "encoded_pointcloud" and len(data) <= len(POINTCLOUD_HEADER):
                 continue
-            _atomic(path, _write_bytes, data)
+            _atomic(path, _write_bytes, data, sink=sink)
             continue
         a = [arrays[x][k] for x in keys]
         if kind == "pointcloud" and np.isnan(a[0]).all():   # no point: no file (GDP:723-725, :1755)
             continue
         if kind == "png":
-            _atomic(path, _write_png, *a)
+            _atomic(path, _write_png, *a, sink=sink)
         elif kind == "npy":
-            _atomic(path, fileio.write_npy, *a)
+            _atomic(path, fileio.write_npy, *a, sink=sink)
         elif kind == "csv":
-            _atomic(path, fileio.write_depth_csv, *a)
+            _atomic(path, fileio.write_depth_csv, *a, sink=sink)
         elif kind == "pointcloud":
-            _atomic(path, fileio.write_pointcloud_txt, *a)
+            _atomic(path, fileio.write_pointcloud_txt, *a, sink=sink)
         else:
             raise ValueError(kind)
     if callable(label):   # a native label writer job (writers.LabelWriter.write bound to the frame)
-        _atomic(label_path, label)
+        _atomic(label_path, label, sink=sink)
     else:
-        _atomic(label_path, _write_bytes, label_json_bytes(label))
+        _atomic(label_path, _write_bytes, label_json_bytes(label), sink=sink)
     return fileio.depth_stats(arrays["depth"][k]) if "depth" in arrays else None
 
 
@@ -124,8 +132,8 @@ def _views(shm_name: str, slot_bytes: int, layout: Layout, slot: int) -> Dict[st
             for k, (off, shape, dt) in layout.items()}
 
 
-def _task(shm_name, slot_bytes, layout, slot, k, files, label, label_path):
-    return write_frame(_views(shm_name, slot_bytes, layout, slot), k, files, label, label_path)
+def _task(shm_name, slot_bytes, layout, slot, k, files, label, label_path, sink):
+    return write_frame(_views(shm_name, slot_bytes, layout, slot), k, files, label, label_path, sink)
 
 
 def _ping() -> int:
@@ -138,8 +146,12 @@ class WriterPool:
     one batch, Renderer.output_spec) and ``workers`` writer processes (mode
     "process") or threads (mode "thread")."""
 
-    def __init__(self, spec: Dict[str, tuple], workers: int, n_slots: int = 3, mode: str = "process"):
+    def __init__(self, spec: Dict[str, tuple], workers: int, n_slots: int = 3, mode: str = "process",
+                 sink: str = "disk"):
+        if sink not in SINKS:
+            raise ValueError(f"sink {sink!r}: choose from {SINKS}")
         self.mode = mode
+        self.sink = sink
         self.workers = workers
         self.task_s, self.tasks = 0.0, 0   # thread mode: summed wall time of the frame tasks
         self.layout: Layout = {}
@@ -178,7 +190,7 @@ class WriterPool:
         self.free = free
         self._grow_lock = threading.Lock()
         self._files_free = {}          # slot -> free() of its current files buffer's renderer
-        self._retired = []             # (replaced files buffer, its free()), released in close()
+        self._retired = []             # (replaced files buffer, its free()): release_retired() / close()
         for slot in range(self.n_slots):
             buf = alloc(self.slot_bytes)
             d = {k: np.ndarray(shape, np.dtype(dt), buffer=buf, offset=off)
@@ -193,9 +205,11 @@ class WriterPool:
         fit), from ``alloc`` / to be released by ``free``: the growing
         renderer's own (Renderer.host_buffer / free_host_buffer), so a
         renderer context is only touched by the thread that renders with it.
-        The replaced buffer is retired, not freed: it is released in
-        :meth:`close`, after every render thread has finished (hipHostFree
-        waits for the device, which would stall the other renderer's batch).
+        The replaced buffer is retired, not freed here (hipHostFree waits
+        for the device, which would stall the other renderer's batch in the
+        middle of this one's copy): its owning renderer's thread releases it
+        at its next batch (:meth:`release_retired`), and :meth:`close` releases
+        whatever is left, so pinned memory does not pile up over a run.
         The lock orders concurrent grows of the renderers' threads."""
         alloc = alloc or self.alloc
         with self._grow_lock:
@@ -207,6 +221,25 @@ class WriterPool:
                     self._retired.append((old, owner))
             self._files_free[slot] = free or self.free
         return self._local[slot]["files"]
+
+    def release_retired(self, free) -> int:
+        """Free the retired files buffers whose owner is ``free`` (the calling
+        render thread's Renderer.free_host_buffer); returns how many.  A
+        retired buffer is no longer any slot's, and the tasks that read it
+        finished before its slot was handed out again (:meth:`arrays`)."""
+        if not getattr(self, "_retired", None):
+            return 0
+        with self._grow_lock:
+            mine = [a for a, f in self._retired if f == free]
+            self._retired = [(a, f) for a, f in self._retired if f != free]
+        for a in mine:
+            free(a)
+        return len(mine)
+
+    @property
+    def retired(self) -> int:
+        """Files buffers replaced by a grow and not yet released."""
+        return len(getattr(self, "_retired", []))
 
     def arrays(self, slot: int) -> Dict[str, np.ndarray]:
         """The slot's arrays, to render into (waits until no task reads it)."""
@@ -222,9 +255,9 @@ class WriterPool:
     def submit(self, slot: int, k: int, files, label: dict, label_path: str) -> Future:
         if self.shm is not None:
             f = self.pool.submit(_task, self.shm.name, self.slot_bytes, self.layout, slot, k, files, label,
-                                 label_path)
+                                 label_path, self.sink)
         else:
-            f = self.pool.submit(self._timed_write, self._local[slot], k, files, label, label_path)
+            f = self.pool.submit(self._timed_write, self._local[slot], k, files, label, label_path, self.sink)
         self.busy[slot].append(f)
         return f
 

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define CSG_ABI_VERSION 10
+#define CSG_ABI_VERSION 11
 
 typedef enum {
   CSG_OK = 0,
@@ -283,9 +283,11 @@ int csg_host_free(csg_ctx* ctx, void* p);
  * and frees the work buffers (the next batch allocates them).  The counts are
  * a pure function of the frame and the scene, so batches that render the
  * measured frames, in that order, with their hints, never overflow.  Other
- * batches can: csg_render_batch then renders again without hints (every frame
- * at the per-frame caps), then with grown caps; an asynchronous batch reports
- * CSG_ERR_OVERFLOW at the next csg_synchronize.  Waits for the context's
+ * batches can: csg_render_batch then renders again -- with the pools grown to
+ * the largest launch chain's hinted total when the frames were grouped
+ * differently, else without hints (every frame at the per-frame caps), then
+ * with grown caps -- and prints a "[csg]" line on stderr for each such retry;
+ * an asynchronous batch reports CSG_ERR_OVERFLOW at the next csg_synchronize.  Waits for the context's
  * earlier batches first (and reports their errors). */
 typedef struct {
   uint32_t records_per_frame;  /* current per-frame caps (frames without hints) */
@@ -300,7 +302,7 @@ typedef struct {
   uint64_t pool_records;       /* pool entries of one launch chain */
   uint64_t pool_bins;
   uint32_t hinted;             /* 1: pools sized from frame hints (csg_size_work) */
-  uint32_t pad;
+  uint32_t hint_retries;       /* re-renders the hinted pools caused (grown pools or hints turned off) */
 } csg_work_info;
 int csg_size_work(csg_ctx* ctx, csg_frame* frames, uint32_t n_frames, int32_t frames_on_device,
                   float margin, csg_work_info* out);

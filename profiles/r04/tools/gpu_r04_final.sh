@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r04
 mkdir -p $O
-TEST=1 PROF=1 BENCH_ARGS="" bash tools/gpu_r04_main.sh || exit 1
+TEST=1 PROF=1 BENCH_ARGS="" bash profiles/r04/tools/gpu_r04_main.sh || exit 1
 timeout -k 10 600 python bench.py --frames-per-step 960 --pcie-steps 0 --stats-steps 0 --verify-frames 8 > $O/bench_C3_960.json 2> $O/bench_C3_960.err || { tail -5 $O/bench_C3_960.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_C3_960.json')); print('C3@960', d['value'], d['work']['bytes'], d['verified']['bit_exact'])" || exit 1
-WORKLOADS="C2 C4 C5" bash tools/gpu_r04_configs.sh
+WORKLOADS="C2 C4 C5" bash profiles/r04/tools/gpu_r04_configs.sh

@@ -116,6 +116,9 @@ def test_shard_report_single_rank_and_gloo_pair(tmp_path):
     import json
     rep = json.load(open(tmp_path / "rep.json"))
     assert rep["disjoint"] and rep["union"] == 2 * 3 * 20 and rep["epochs_mod_world"] == [[0], [1]]
+    # two ranks on the one device of a rehearsal box say so
+    assert [d["rank"] for d in rep["devices"]] == [0, 1]
+    assert rep["distinct_devices"] == 1 and rep["shared_devices"] is True
 
 
 def _shard_worker(rank, port, out_dir):
@@ -126,11 +129,88 @@ def _shard_worker(rank, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=2)
     fids = bench.rank_frames(rank, 2, 4, 20)
-    rep = bench.shard_report(bench.timed_frames(fids, 1, 3, 20), 2)
+    dev = {"rank": rank, "local_rank": rank, "device": 0, "device_count": 1, "pci": "0000:05:00"}
+    rep = bench.shard_report(bench.timed_frames(fids, 1, 3, 20), 2, dev)
     if rank == 0:
         json.dump(rep, open(os.path.join(out_dir, "rep.json"), "w"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+_CHILD = r"""
+import os, sys, time
+r, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+assert os.environ["LOCAL_RANK"] == str(r) and os.environ["MASTER_ADDR"] == "127.0.0.1"
+assert int(os.environ["MASTER_PORT"]) > 0
+mode = sys.argv[1]
+if mode == "fail" and r == n - 1:
+    sys.stderr.write("rank failing on purpose\n")
+    sys.exit(7)
+if mode == "crash" and r == 1:
+    os.kill(os.getpid(), 9)
+if mode in ("fail", "crash", "hang"):
+    time.sleep(120 if mode == "hang" or r == 0 else 0)   # the others wait: they must be stopped
+print("noise that is not a result line")
+if r == 0:
+    print('{"n_gpus": %d, "rank": 0}' % n, flush=True)
+"""
+
+
+def _launch(mode, n, tmp_path):
+    import io
+    import time as _t
+    script = tmp_path / "child.py"
+    script.write_text(_CHILD)
+    buf = io.StringIO()
+    t0 = _t.time()
+    rc = bench.launch_ranks(n, [sys.executable, str(script), mode], env=dict(os.environ), out=buf,
+                            poll_s=0.05, grace_s=5.0)
+    return rc, buf.getvalue(), _t.time() - t0
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_launcher_forwards_rank0_line(tmp_path, n):
+    """A plain `bench.py --gpus N` starts N ranks itself: each child sees its
+    RANK / LOCAL_RANK and the shared WORLD_SIZE / MASTER_*, and only rank 0's
+    JSON line is forwarded."""
+    env_before = dict(os.environ)
+    rc, out, _ = _launch("ok", n, tmp_path)
+    assert rc == 0
+    assert out.splitlines() == ['{"n_gpus": %d, "rank": 0}' % n]
+    assert dict(os.environ) == env_before          # the parent's environment is untouched
+
+
+@pytest.mark.parametrize("mode,code", [("fail", 7), ("crash", 1)])
+def test_launcher_failing_child_gives_no_line(tmp_path, mode, code):
+    """Any failing rank -- an error exit, or a rank killed by a signal --
+    stops the other ranks (rank 0 sleeps 120 s here), and the launcher exits
+    non-zero without printing a line."""
+    rc, out, dt = _launch(mode, 3, tmp_path)
+    assert rc == code and out == ""
+    assert dt < 60
+
+
+def test_bench_main_launches_ranks_without_torchrun(tmp_path, monkeypatch):
+    """`main()` with --gpus 2 and no WORLD_SIZE hands over to launch_ranks
+    before importing torch, passing its own arguments to the children."""
+    seen = {}
+
+    def fake(n, argv, **kw):
+        seen["n"], seen["argv"] = n, argv
+        return 5
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "launch_ranks", fake)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 5 and seen["n"] == 2
+    assert seen["argv"][0] == sys.executable and seen["argv"][1].endswith("bench.py")
+    assert seen["argv"][2:] == ["--gpus", "2", "--steps", "3"]
+
+
+def test_shard_report_devices():
+    r = bench.shard_report([1, 2], 1, {"rank": 0, "local_rank": 0, "device": 0, "device_count": 1, "pci": "0000:05:00"})
+    assert r["devices"][0]["pci"] == "0000:05:00" and r["distinct_devices"] == 1 and r["shared_devices"] is False
 
 
 @pytest.mark.parametrize("steps,warmup", [(20, 5), (10, 2), (200, 10)])

@@ -56,6 +56,36 @@ def test_bench_two_ranks_under_torchrun(tmp_path):
     assert abs(d["value"] - 2 * steps * F / (d["ms_per_step"] * steps / 1e3)) <= 0.01 * d["value"]
 
 
+@pytest.mark.timeout(900)
+def test_bench_two_ranks_plain_command(tmp_path):
+    """`python3 bench.py --gpus 2` with no torchrun and no rank environment:
+    bench.py starts its two ranks itself (fresh child processes, before any
+    GPU call) and forwards rank 0's line, which reports both ranks, their
+    devices (here both on the box's one GPU: `shared_devices`), disjoint
+    shards and the oracle check."""
+    steps, warmup, F = 2, 1, 48
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup",
+           str(warmup), "--frames-per-step", str(F), "--verify-frames-multi", "4"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    log = tmp_path / "bench2plain.err"
+    with open(log, "w") as err:
+        r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=err, text=True, timeout=840)
+    tail = log.read_text()[-4000:]
+    assert r.returncode == 0, f"plain bench --gpus 2 failed ({r.returncode}):\n{tail}"
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["verified"]["frames"] == 8 and d["verified"]["bit_exact"] is True
+    sh = d["shards"]
+    assert sh["ranks"] == 2 and sh["disjoint"] is True and sh["union"] == 2 * steps * F
+    assert [x["rank"] for x in sh["devices"]] == [0, 1]
+    ndev = sh["devices"][0]["device_count"]
+    assert all(x["device_count"] == ndev for x in sh["devices"])
+    assert sh["shared_devices"] is (ndev < 2)
+    assert sh["distinct_devices"] == min(2, ndev)
+
+
 @pytest.mark.timeout(600)
 def test_bench_single_rank_every_leg_with_hinted_pools(tmp_path):
     """N = 1 with two launch chains per step: the sizing pass's hints and

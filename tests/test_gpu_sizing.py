@@ -12,8 +12,9 @@ record / bin pools planned per launch chain.
   at csg_synchronize, and the context renders correctly afterwards;
 * pools smaller than a chain of per-frame caps: hinted frames rendered in the
   sized order, in chains, never overflow; a chain of the heaviest frames that
-  exceeds the pool is reported (asynchronous) or rendered again without hints
-  (synchronous), bit-exact either way.
+  exceeds the pool is reported (asynchronous) or rendered again with grown
+  pools (synchronous), and frames with stale hints again without hints,
+  bit-exact every time.
 """
 import numpy as np
 import pytest
@@ -171,12 +172,26 @@ def test_hinted_pools_chains_and_reordered_heavy_chain():
         torch.cuda.synchronize(dev)
         with pytest.raises(CsgError, match="overflow"):
             r.synchronize()
-        # synchronous: rendered again without hints, bit-exact; hints stay off
+        # synchronous: the chain's hints add up past the pool (a grouping the
+        # sizing did not see: k_plan's need[]), so the pools grow to that chain
+        # and the batch renders again with its hints, bit-exact
         got = r.render(hv, want=("rgb", "instance"))
         assert np.array_equal(got["rgb"], ref["rgb"][heavy])
         assert np.array_equal(got["instance"], ref["instance"][heavy])
         wi = r.work_info()
-        assert wi["hinted"] == 0 and wi["records_per_frame"] == info["records_per_frame"]
+        assert wi["hinted"] == 1 and wi["hint_retries"] == 1
+        assert wi["pool_records"] >= int(rh[heavy].sum())
+        # stale hints (every frame far below its count): the chain fits the
+        # pool but each frame overflows its own slab, so hints go off and the
+        # frames render at the per-frame caps, bit-exact
+        stale = hv.copy()
+        stale["records_hint"] = 64
+        got = r.render(stale, want=("rgb", "instance"))
+        assert np.array_equal(got["rgb"], ref["rgb"][heavy])
+        assert np.array_equal(got["instance"], ref["instance"][heavy])
+        wi = r.work_info()
+        assert wi["hinted"] == 0 and wi["hint_retries"] == 2
+        assert wi["records_per_frame"] == info["records_per_frame"]
 
 
 def test_hinted_pools_c5_4k_every_output():

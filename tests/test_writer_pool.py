@@ -94,6 +94,29 @@ def test_grown_files_buffers_are_retired_until_close():
     assert [e for e in events if e[0] == "free"] == [("free", "r0", 100), ("free", "r1", 200)]
 
 
+def test_retired_files_buffers_released_by_their_renderer():
+    """Repeated grows do not pile up pinned memory: each renderer's thread
+    releases the buffers it owns at its next batch (release_retired), the
+    other renderer's stay until theirs, and close() frees the rest."""
+    from constructionsceneposeestimation_amd.writer_pool import WriterPool
+    freed = []
+    free0 = lambda a: freed.append(("r0", a.nbytes))   # noqa: E731
+    free1 = lambda a: freed.append(("r1", a.nbytes))   # noqa: E731
+    pool = WriterPool({"rgb": ((1, 4, 4, 3), np.uint8)}, workers=1, n_slots=3, mode="thread")
+    pool.use_pinned(lambda n: np.zeros(n, np.uint8), files_bytes=100, free=free0)
+    size = 100
+    for k in range(6):   # renderers alternate; slot k % 3 grows 1.25x each time
+        size = size * 5 // 4
+        own = free0 if k % 2 == 0 else free1
+        pool.release_retired(own)          # the renderer's next batch starts
+        pool.grow_files(k % 3, size, alloc=lambda n: np.zeros(n, np.uint8), free=own)
+        assert pool.retired <= 2           # at most the other renderer's last grow and this one
+    assert pool.retired == 1 and len(freed) == 5   # r0's last replaced buffer waits for r0's next batch
+    assert pool.release_retired(free1) == 0        # not r1's
+    pool.close()
+    assert pool.retired == 0 and len(freed) == 6   # every replaced buffer released exactly once
+
+
 def test_frames_without_points_get_no_pointcloud_file(tmp_path):
     """The reference writes no point-cloud file for a frame without a single
     point (save_pointcloud_with_rgb returns on an empty cloud, GDP:723-725;
@@ -115,3 +138,29 @@ def test_frames_without_points_get_no_pointcloud_file(tmp_path):
     pts[0, 1, 1] = (1.0, 2.0, 3.0)
     write_frame(arrays, 0, [(p[3], "pointcloud", ("points", "rgb"))], {"frame_id": 0}, str(tmp_path / "l1.json"))
     assert open(p[3], "rb").read() == POINTCLOUD_HEADER + b"1.000000 2.000000 3.000000 0.000000 0.000000 0.000000\n"
+
+
+@pytest.mark.parametrize("mode", ["thread", "process"])
+def test_discard_sink_writes_no_files(tmp_path, mode):
+    """Sink "discard" (generate --sink discard, the steady-state measurement)
+    runs every writer -- PNG, npy, CSV, label JSON -- into /dev/null: the
+    same work, no file left behind, and the same depth counts."""
+    from constructionsceneposeestimation_amd.writer_pool import WriterPool
+    H, W, n = 12, 20, 2
+    spec = {"rgb": ((n, H, W, 3), np.uint8), "instance": ((n, H, W), np.int32), "depth": ((n, H, W), np.float32)}
+    pool = WriterPool(spec, workers=2, n_slots=1, mode=mode, sink="discard")
+    try:
+        arrays = pool.arrays(0)
+        _fill(arrays, n, np.random.default_rng(1))
+        futs = [pool.submit(0, k, [(str(tmp_path / f"rgb_{k}.png"), "png", ("rgb",)),
+                                   (str(tmp_path / f"mask_{k}.npy"), "npy", ("instance",)),
+                                   (str(tmp_path / f"depth_{k}.csv"), "csv", ("depth",))],
+                            {"frame_id": k}, str(tmp_path / f"label_{k}.json")) for k in range(n)]
+        stats = [f.result() for f in futs]
+        del arrays
+    finally:
+        pool.close()
+    assert all(s["total"] == H * W and s["inf"] == 2 * W for s in stats)
+    assert not list(tmp_path.iterdir())
+    with pytest.raises(ValueError):
+        WriterPool(spec, workers=1, n_slots=1, mode="thread", sink="nowhere")
