@@ -1112,6 +1112,21 @@ __device__ __forceinline__ int cov_find(const RasterCtx& c, uint32_t label) {
 
 __device__ __forceinline__ float f_(uint32_t u) { return __uint_as_float(u); }
 
+// Z-buffer word of tile pixel (lx, ly): row-major with the column XORed by
+// the row (CSG_ZB_SWIZZLE).  A row-major tile of 8-B words puts every row on
+// the same LDS banks, so fragments at one column of a stack of rows (a small
+// record's rows, vertically aligned spans) and the resolve's 4-pixel groups
+// (lanes t and t+8 of a lane group 32 B x 8 apart) met on one bank pair
+// (profiles/r05/ab/lds_counters.txt).  XORing the column with the row keeps
+// each row a permutation of its words (consecutive pixels of a span stay
+// distinct) and each aligned 4-pixel group inside its own 32 B.
+#ifndef CSG_ZB_SWIZZLE
+#define CSG_ZB_SWIZZLE 1
+#endif
+__device__ __forceinline__ int zb_index(int lx, int ly) {
+  return ly * kTileW + (CSG_ZB_SWIZZLE ? (lx ^ (ly & (kTileW - 1))) : lx);
+}
+
 // One fragment of staged record k at tile pixel (lx, ly), already known to be
 // covered: homogeneous depth, depth range, early-z against the LDS key,
 // alpha test (texture described inline in the record), then ds_min_u64.
@@ -1133,7 +1148,7 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
     return alpha_pass(c.aquad, c.acls, (g2.y & 0xFFFFFFu) * kTexAlign, g4.w, (int)(g2.y >> 24), uv.x, uv.y);
   };
   const unsigned long long key = ((unsigned long long)(0xFFFFFFFFu - fbits(invw)) << 32) | g2.x;
-  unsigned long long* z = &c.zb[ly * kTileW + lx];
+  unsigned long long* z = &c.zb[zb_index(lx, ly)];
   if constexpr (kCov) {
     // A fragment has two possible effects: its label's coverage bit and the
     // depth minimum.  One that loses early-z and whose bit is already set has
@@ -1756,7 +1771,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
       const uint32_t pp = b.kp_pix[o];
       const int px = (int)(pp & 0xFFFFu) - ox, py = (int)(pp >> 16) - oy;
       if (pp == 0xFFFFFFFFu || px < 0 || px >= kTileW || py < 0 || py >= kTileH) continue;
-      const unsigned long long key = zb[py * kTileW + px];
+      const unsigned long long key = zb[zb_index(px, py)];
       const float d = key == kEmptyKey ? INFINITY : rcp_ieee(__uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32)));
       b.kp_vis[o] = (b.kp_w[o] <= d) ? 2 : 1;
     }
@@ -1789,7 +1804,11 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
   const int py = oy + ly;
   const bool row_ok = py < (int)s.H;
   const int px0 = ox + lx0;
-  unsigned long long* zrow = &zb[ly * kTileW + lx0];
+  // this thread's 4 pixels: the aligned 4-word group at zb_index(lx0, ly) & ~3,
+  // pixel k in word k ^ (ly & 3) of it (zpix)
+  unsigned long long* zrow = &zb[zb_index(lx0, ly) & ~3];
+  const int zsw = CSG_ZB_SWIZZLE ? (ly & 3) : 0;
+  auto zpix = [&](int k) -> unsigned long long& { return zrow[k ^ zsw]; };
   uint32_t pend = 0;                 // bit k: pixel k still to shade
   uint32_t inmask = 0;               // bit k: pixel k lies inside the frame
   // The depth visualisation's range (b.drange), from the winning keys: the
@@ -1805,13 +1824,13 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
     for (int k = 0; k < 4; ++k) {
       const bool in = row_ok && px0 + k < (int)s.W;
       inmask |= in ? 1u << k : 0u;
-      const unsigned long long key = zrow[k];
+      const unsigned long long key = zpix(k);
       if (in && key != kEmptyKey) {
         pend |= 1u << k;
         kmn = min(kmn, (uint32_t)(key >> 32));
         kmx = max(kmx, (uint32_t)(key >> 32));
       } else {
-        zrow[k] = bgword;            // background (or outside the frame)
+        zpix(k) = bgword;            // background (or outside the frame)
       }
     }
     if (b.drange) {
@@ -1857,7 +1876,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if ((pend >> k) & 1u) {
-          const uint32_t uid = (uint32_t)zrow[k];
+          const uint32_t uid = (uint32_t)zpix(k);
           uint32_t sl;
           if (uid == prev_uid) sl = prev_slot;
           else {
@@ -1931,7 +1950,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
           shade_pixel(s, e, px, qy, need_depth, rgb, id, dep);
           n01 = e.n01;
           n2 = e.n2;
-          zrow[k] = (unsigned long long)rgb | ((unsigned long long)(uint32_t)id << 32);
+          zpix(k) = (unsigned long long)rgb | ((unsigned long long)(uint32_t)id << 32);
           pend &= ~(1u << k);
           if (want_stats) {
             if (id != run) {
@@ -1977,7 +1996,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
     int32_t ids[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const unsigned long long w = zrow[k];
+      const unsigned long long w = zpix(k);
       rgb[k] = (uint32_t)w;
       ids[k] = (int32_t)(w >> 32);
     }

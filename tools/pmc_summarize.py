@@ -12,7 +12,8 @@ import os
 import sys
 from collections import defaultdict
 
-N_SIMD = 256 * 4    # MI355X: 256 CUs x 4 SIMDs
+N_CU = 256
+N_SIMD = N_CU * 4   # MI355X: 256 CUs x 4 SIMDs
 N_XCD = 8
 
 
@@ -67,6 +68,15 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
             o["valu_busy"] = o["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / (o["GRBM_GUI_ACTIVE"] / N_XCD)
             if "SQ_THREAD_CYCLES_VALU" in o and o["SQ_ACTIVE_INST_VALU"] > 0:
                 o["valu_lane_util"] = o["SQ_THREAD_CYCLES_VALU"] / (o["SQ_ACTIVE_INST_VALU"] * 64)
+        if "SQ_LDS_IDX_ACTIVE" in o and o["SQ_LDS_IDX_ACTIVE"] > 0:
+            # LDS-array cycles (summed over the 256 CUs) and the extra cycles bank conflicts
+            # added to them (MI355X_MICROARCH.md §LDS): conflict share and LDS busy per CU
+            if "SQ_LDS_BANK_CONFLICT" in o:
+                o["lds_conflict_share"] = o["SQ_LDS_BANK_CONFLICT"] / o["SQ_LDS_IDX_ACTIVE"]
+            if "GRBM_GUI_ACTIVE" in o and o["GRBM_GUI_ACTIVE"] > 0:
+                o["lds_busy"] = o["SQ_LDS_IDX_ACTIVE"] / N_CU / (o["GRBM_GUI_ACTIVE"] / N_XCD)
+        if "SQ_WAIT_INST_LDS" in o and o.get("SQ_WAVE_CYCLES"):
+            o["lds_wait_share"] = o["SQ_WAIT_INST_LDS"] / o["SQ_WAVE_CYCLES"]
     print(json.dumps(out, indent=1, sort_keys=True))
     if write_profile and "k_raster" in out and "hbm_bytes_per_launch" in out["k_raster"]:
         # the bench line of a pass names the workload, frames per launch and B_frame it ran
