@@ -187,7 +187,12 @@ struct csg_ctx {
   hipEvent_t* ev = nullptr;             // events of the most recent batch
   uint32_t last_F = 0;
   uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
-  uint32_t bin_blocks = 32;             // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only)
+  // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only).  16 at the
+  // 32 x 16 tiles keeps the [blocks][tiles] count grid the size 32 blocks gave
+  // 32 x 32 tiles (C3 32 x 16: binning 2.27 vs 2.69 ms per 960 frames with 16 vs
+  // 32 blocks; at 2,880 frames per step 8 / 16 / 24 blocks: binning 5.8 / 6.2 /
+  // 6.3 ms, k_raster 97.3 / 97.1 / 96.9 ms; profiles/r05/ab/tile_shape.md)
+  uint32_t bin_blocks = kTileH >= 32 ? 32 : 16;
   uint32_t chain_frames = 0;            // frames per launch chain (cfg.frames_per_launch; CSG_CHAIN overrides)
   // the last sizing pass (csg_size_work)
   uint32_t sized_frames = 0, sized_max_rec = 0, sized_max_bin = 0;

@@ -7,14 +7,16 @@
 namespace csg {
 
 // Screen tiles: one k_raster workgroup each, 4 consecutive pixels of a tile
-// row per thread in the resolve.  32 x 32 (1,024 pixels, 256 threads) is the
-// production shape; CSG_TILE_W / CSG_TILE_H build the other shapes measured
-// against it (profiles/r05/ab/tile_shape.txt).
+// row per thread in the resolve.  32 x 16 (512 pixels, 128-thread / 2-wave
+// workgroups) is the production shape since round 5: against 32 x 32 (256
+// threads) k_raster -1.8%, frames/s +0.7% with 16 binning blocks per frame
+// (C3, 2,880 frames per step; 64 x 16 +3.7%, 16 x 16 +17% raster;
+// profiles/r05/ab/tile_shape.md).  CSG_TILE_W / CSG_TILE_H build the others.
 #ifndef CSG_TILE_W
 #define CSG_TILE_W 32
 #endif
 #ifndef CSG_TILE_H
-#define CSG_TILE_H 32
+#define CSG_TILE_H 16
 #endif
 constexpr int kTileW = CSG_TILE_W;           // tile width (pixels)
 constexpr int kTileH = CSG_TILE_H;           // tile height (pixels)
@@ -27,10 +29,10 @@ constexpr int kBlock = 256;
 constexpr uint32_t kUidShift = 20;        // spec: uid = (instance << 20) | triangle (tie order); see SceneDev::uid_shift
 constexpr uint32_t kMaxInstances = 1u << (32 - kUidShift);
 constexpr uint32_t kMaxTrisPerMesh = 1u << kUidShift;
-#ifndef CSG_LDS_LABELS
-#define CSG_LDS_LABELS 256
+#ifndef CSG_LDS_LABELS   // per-label pixel stats kept in k_raster's LDS (the rest: global atomics)
+#define CSG_LDS_LABELS ((CSG_TILE_W) * (CSG_TILE_H) >= 1024 ? 256 : 64)   // C3-C5 have 45 labels
 #endif
-constexpr int kMaxLdsLabels = CSG_LDS_LABELS;   // per-label pixel stats kept in LDS (the rest: global atomics)
+constexpr int kMaxLdsLabels = CSG_LDS_LABELS;
 constexpr int kCovSlots = 32;             // labels per tile in k_raster's coverage table (occlusion)
 constexpr uint32_t kCovUnknown = 0x80000000u;   // covered[] flag: a tile held more than kCovSlots labels
 constexpr uint32_t kCounterStride = 64;   // u32s between per-frame counters: one 256-B line each

@@ -1020,14 +1020,17 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // further -4%, 8 waves lose again to spills and small batches).  Seven
 // 256-thread workgroups per CU need <= 22 KiB of LDS each (124 staged 80-B
 // records, 116 shade-table slots) and <= 72 VGPRs.
+// Per tile shape (workgroup size): 124 staged records / 116 shade slots for
+// 256-thread workgroups (32 x 32), 60 / 64 for 128-thread ones (32 x 16);
+// either way 7 waves per SIMD fit the LDS and the 72-VGPR budget.
 #ifndef CSG_STAGE
-#define CSG_STAGE 124
+#define CSG_STAGE (kRasterBlock >= 256 ? 124 : 60)
 #endif
 #ifndef CSG_WAVES
 #define CSG_WAVES 7             // k_raster waves per SIMD to budget registers for
 #endif
-#ifndef CSG_COV_STAGE
-#define CSG_COV_STAGE 72        // k_raster<true>: smaller batches pay for the coverage table (7 workgroups per CU)
+#ifndef CSG_COV_STAGE          // k_raster<true>: smaller batches pay for the coverage table (7 waves per SIMD)
+#define CSG_COV_STAGE (kRasterBlock >= 256 ? 72 : 32)
 #endif
 #ifndef CSG_COV_WAVES
 #define CSG_COV_WAVES 7
@@ -1560,7 +1563,7 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
 // triangles in an open-addressing table of kShadeSlots, each set up once by
 // one thread, then read by every pixel that shows it.
 #ifndef CSG_SHADE_SLOTS
-#define CSG_SHADE_SLOTS 116
+#define CSG_SHADE_SLOTS (kRasterBlock >= 256 ? 116 : 64)
 #endif
 constexpr uint32_t kShadeSlots = CSG_SHADE_SLOTS;   // <= kRasterBlock (one setup thread per slot)
 static_assert(kShadeSlots <= (uint32_t)kRasterBlock && kShadeSlots < 255u, "one setup thread per slot; 8-bit slot ids");

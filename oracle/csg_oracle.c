@@ -159,8 +159,10 @@ static inline void interp_uv(const hom_t* h, int px, int py, float invw, float* 
 
 /* Label coverage for occlusion: per label, the pixels a
  * fragment of it covers (centre covered, depth in range, alpha test passed;
- * no depth test), and per 32x32 tile the labels that have such a fragment. */
-#define COV_TILE 32
+ * no depth test), and per 32x16 tile (k_raster's tile since round 5) the
+ * labels that have such a fragment. */
+#define COV_TILE_W 32
+#define COV_TILE_H 16
 #define COV_SLOTS 32
 #define COV_UNKNOWN 0x80000000u
 typedef struct {
@@ -240,7 +242,7 @@ static void raster_tri(const oracle_scene* s, uint64_t* zbuf, const float su[3],
         if (lab >= 0 && (uint32_t)lab < cv->n_labels && alpha_passes(s, mat, h, px, py, invw)) {
           const size_t bit = (size_t)lab * W * H + (size_t)py * W + px;
           cv->bits[bit >> 3] |= (uint8_t)(1u << (bit & 7));
-          cv->tile[((size_t)(py / COV_TILE) * cv->tiles_x + px / COV_TILE) * cv->n_labels + lab] = 1;
+          cv->tile[((size_t)(py / COV_TILE_H) * cv->tiles_x + px / COV_TILE_W) * cv->n_labels + lab] = 1;
         }
       }
       const uint64_t key = ((uint64_t)(0xFFFFFFFFu - fbits(invw)) << 32) | uid;
@@ -342,8 +344,8 @@ static void cov_finish(const cov_t* cv, int W, int H, uint32_t* covered) {
         if (!tl[l]) continue;
         if (n > COV_SLOTS) { covered[l] |= COV_UNKNOWN; continue; }
         uint32_t cnt = 0;
-        for (int py = (int)ty * COV_TILE; py < (int)(ty + 1) * COV_TILE && py < H; ++py)
-          for (int px = (int)tx * COV_TILE; px < (int)(tx + 1) * COV_TILE && px < W; ++px) {
+        for (int py = (int)ty * COV_TILE_H; py < (int)(ty + 1) * COV_TILE_H && py < H; ++py)
+          for (int px = (int)tx * COV_TILE_W; px < (int)(tx + 1) * COV_TILE_W && px < W; ++px) {
             const size_t bit = (size_t)l * W * H + (size_t)py * W + px;
             cnt += (cv->bits[bit >> 3] >> (bit & 7)) & 1u;
           }
@@ -363,8 +365,8 @@ int oracle_render_frame_cov(const oracle_scene* s, const float* view, const floa
   cov_t cov_store, *cv = NULL;
   if (label_covered && n_labels) {
     cov_store.n_labels = n_labels;
-    cov_store.tiles_x = (uint32_t)(W + COV_TILE - 1) / COV_TILE;
-    cov_store.tiles_y = (uint32_t)(H + COV_TILE - 1) / COV_TILE;
+    cov_store.tiles_x = (uint32_t)(W + COV_TILE_W - 1) / COV_TILE_W;
+    cov_store.tiles_y = (uint32_t)(H + COV_TILE_H - 1) / COV_TILE_H;
     cov_store.bits = (uint8_t*)calloc(((size_t)n_labels * W * H + 7) / 8, 1);
     cov_store.tile = (uint8_t*)calloc((size_t)cov_store.tiles_x * cov_store.tiles_y * n_labels, 1);
     if (!cov_store.bits || !cov_store.tile) {

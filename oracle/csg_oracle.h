@@ -83,7 +83,7 @@ int oracle_render_frame_ex(const oracle_scene* s, const float* view, const float
 
 /* Same plus the label coverage of the occlusion ratio: label_covered
  * [n_labels] = pixels each label covers with a fragment in the depth range
- * that passes its alpha test (no depth test); a 32x32 tile with more than 32
+ * that passes its alpha test (no depth test); a 32x16 tile with more than 32
  * such labels flags them with bit 31 and adds no counts. */
 int oracle_render_frame_cov(const oracle_scene* s, const float* view, const float* proj,
                             uint8_t* rgb, int32_t* inst, float* depth, uint16_t* normals, float* points,

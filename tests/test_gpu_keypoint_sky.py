@@ -29,13 +29,13 @@ def test_keypoints_over_sky_in_mixed_tiles_are_visible_every_time():
     o.set_instance_models(st.models.reshape(-1, 16))
     depth = o.render(V[0], P[0])["depth"]
     sky = ~np.isfinite(depth)
-    # sky pixels of 32x32 tiles that also hold geometry
+    # sky pixels of k_raster tiles (32x16) that also hold geometry
     mixed = np.zeros_like(sky)
-    for ty in range(0, H, 32):
+    for ty in range(0, H, 16):
         for tx in range(0, W, 32):
-            t = sky[ty:ty + 32, tx:tx + 32]
+            t = sky[ty:ty + 16, tx:tx + 32]
             if t.any() and not t.all():
-                mixed[ty:ty + 32, tx:tx + 32] = t
+                mixed[ty:ty + 16, tx:tx + 32] = t
     ys, xs = np.nonzero(mixed)
     assert len(ys) > 400
     pick = np.random.default_rng(0).choice(len(ys), 400, replace=False)

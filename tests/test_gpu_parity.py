@@ -96,7 +96,7 @@ def test_launch_chains(world2):
 
 
 def test_ragged_size_overflow_growth_and_empty_frame(world2):
-    """A frame size that is a multiple of neither the 32-px tile nor the 4-px
+    """A frame size that is a multiple of neither the 32x16 tile nor the 4-px
     store group (partial tiles, per-pixel store paths), work buffers sized far
     too small (csg_render_batch grows them and renders again), and a frame
     that sees nothing (every tile takes the empty-tile path): all outputs,
