@@ -1624,12 +1624,19 @@ __device__ __forceinline__ int shade_slot(uint32_t* keys, uint32_t uid) {
 // square share one L2, so a record binned to several of them is fetched once,
 // while all XCDs keep working side by side on the same part of the frame.
 // Blocks past the frame's edge (odd tile counts) return at once.
-constexpr uint32_t kSq = 2;   // square edge in tiles
+#ifndef CSG_SQ_X
+#define CSG_SQ_X 2
+#endif
+#ifndef CSG_SQ_Y
+#define CSG_SQ_Y 2
+#endif
+constexpr uint32_t kSqX = CSG_SQ_X, kSqY = CSG_SQ_Y;   // a square's edge in tiles (x, y)
+constexpr uint32_t kSqN = kSqX * kSqY;
 __device__ __forceinline__ bool swizzled_tile(uint32_t v, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tile) {
-  const uint32_t sqx = (tiles_x + kSq - 1) / kSq, sqy = (tiles_y + kSq - 1) / kSq;
-  const uint32_t sq = (v / (8u * kSq * kSq)) * 8u + (v & 7u), j = (v >> 3) % (kSq * kSq);
+  const uint32_t sqx = (tiles_x + kSqX - 1) / kSqX, sqy = (tiles_y + kSqY - 1) / kSqY;
+  const uint32_t sq = (v / (8u * kSqN)) * 8u + (v & 7u), j = (v >> 3) % kSqN;
   if (sq >= sqx * sqy) return false;
-  const uint32_t tx = (sq % sqx) * kSq + (j % kSq), ty = (sq / sqx) * kSq + (j / kSq);
+  const uint32_t tx = (sq % sqx) * kSqX + (j % kSqX), ty = (sq / sqx) * kSqY + (j / kSqX);
   if (tx >= tiles_x || ty >= tiles_y) return false;
   tile = ty * tiles_x + tx;
   return true;
@@ -2269,8 +2276,8 @@ void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_
 }
 
 void launch_raster(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
-  const uint32_t squares = ((s.tiles_x + kSq - 1) / kSq) * ((s.tiles_y + kSq - 1) / kSq);
-  dim3 g(8 * kSq * kSq * ((squares + 7) / 8), F);
+  const uint32_t squares = ((s.tiles_x + kSqX - 1) / kSqX) * ((s.tiles_y + kSqY - 1) / kSqY);
+  dim3 g(8 * kSqN * ((squares + 7) / 8), F);
   if (b.covered) hipLaunchKernelGGL(k_raster<true>, g, dim3(kRasterBlock), 0, st, s, b);
   else hipLaunchKernelGGL(k_raster<false>, g, dim3(kRasterBlock), 0, st, s, b);
 }
