@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r05/ab
 mkdir -p $O
 L=$PWD/constructionsceneposeestimation_amd
-ARGS="--steps ${STEPS:-8} --warmup 1 --frames-per-step ${FPS:-960} --pcie-steps 0 --stats-steps 0 --cpu-single-frames 1"
+ARGS="--steps ${STEPS:-8} --warmup 1 --frames-per-step ${FPS:-960} --pcie-steps 0 --stats-steps ${STATS:-0} --cpu-single-frames 1"
 # 1. the counters this GPU's profiler offers
 timeout -s KILL 60 rocprofv3 -L > $O/avail.txt 2>&1 || echo "list-avail failed"
 want="SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_ANY SQ_WAVE_CYCLES"
@@ -25,7 +25,7 @@ for spec in ${VARIANTS:-base s108 w64h16 w32h16 w16h16}; do
   tag=$(echo $spec | tr ':=' '__')
   if [ $v = base ]; then lib=$L/libcsg.so; else lib=$L/libcsg_$v.so; fi
   env CSG_LIB=$lib $envs timeout -k 10 300 python3 bench.py $ARGS --verify-frames 8 > $O/tile_$tag.json 2> $O/tile_$tag.err || { echo "$spec FAILED"; tail -5 $O/tile_$tag.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/tile_$tag.json')); print('$spec rep $rep', d['value'], d['stage_ms_per_step'], 'recs/frame', d['records_per_frame'], 'bins/frame', d['bin_entries_per_frame'], 'exact', d['verified']['bit_exact'], d['verified']['frames'])" | tee -a $O/tile_ab.txt
+  python3 -c "import json; d=json.load(open('$O/tile_$tag.json')); ws=d.get('with_label_stats') or {}; print('$spec rep $rep', d['value'], d['stage_ms_per_step'], 'recs/frame', d['records_per_frame'], 'bins/frame', d['bin_entries_per_frame'], 'exact', d['verified']['bit_exact'], d['verified']['frames'], 'stats', ws.get('value'), 'occl', (ws.get('with_occlusion_and_depth_png') or {}).get('value'))" | tee -a $O/tile_ab.txt
 done
 done
 fi
