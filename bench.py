@@ -724,7 +724,9 @@ def main():
             dt = time.perf_counter() - t1
             pcie = {"value": round(args.pcie_steps * F / dt, 2), "unit": "frames/s",
                     "note": f"outputs (RGB8 + int32 ids + keypoints, {H * Wd * 7 / 1e6:.1f} MB/frame) copied to "
-                            f"pinned host memory inside the timed region; {args.pcie_steps} batches of {F}"}
+                            f"pinned host memory inside the timed region (each launch chain's slice on a copy "
+                            f"stream while the next chains render); {args.pcie_steps} batches of {F}",
+                    "gbs": round(args.pcie_steps * F * H * Wd * 7 / dt / 1e9, 2)}
         except Exception as e:  # the extra figure must never break the bench line
             log(f"pcie-inclusive measurement failed: {e}")
 
@@ -753,7 +755,7 @@ def main():
             "stage_ms_per_step": {k: round(tm[k] / K, 4) for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")},
             "work": {"bytes": int(winfo["work_bytes"]), "contexts": NC,
                      "pool_records": int(winfo["pool_records"]), "pool_bins": int(winfo["pool_bins"]),
-                     "hinted": bool(winfo["hinted"]),
+                     "hinted": bool(winfo["hinted"]), "hint_retries": int(r.work_info()["hint_retries"]),
                      "records_per_frame_cap": int(winfo["records_per_frame"]),
                      "bins_per_frame_cap": int(winfo["bins_per_frame"]),
                      "frames_per_launch": int(winfo["frames_per_launch"]),

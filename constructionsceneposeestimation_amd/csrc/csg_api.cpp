@@ -194,6 +194,12 @@ struct csg_ctx {
   // 6.3 ms, k_raster 97.3 / 97.1 / 96.9 ms; profiles/r05/ab/tile_shape.md)
   uint32_t bin_blocks = kTileH >= 32 ? 32 : 16;
   uint32_t chain_frames = 0;            // frames per launch chain (cfg.frames_per_launch; CSG_CHAIN overrides)
+  // Host outputs: each launch chain's slice is copied to the host on copy_stream
+  // while the next chains render (created with the first host-output batch).
+  static constexpr uint32_t kCopyEv = 16;
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t copy_ev[kCopyEv] = {};
+  hipEvent_t copy_done = nullptr;
   // the last sizing pass (csg_size_work)
   uint32_t sized_frames = 0, sized_max_rec = 0, sized_max_bin = 0;
   double sized_mean_rec = 0.0, sized_mean_bin = 0.0;
@@ -350,6 +356,11 @@ void csg_destroy(csg_ctx* c) {
   }
   for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  for (auto& e : c->copy_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->copy_done) (void)hipEventDestroy(c->copy_done);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -967,10 +978,22 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   }
   SceneDev s = scene_dev(c);
   // The batch runs as consecutive launch chains of `chain_frames` frames (by
-  // default one chain); the work buffers hold one chain.
-  const uint32_t G = c->chain_frames;
+  // default one chain); the work buffers hold one chain.  With host outputs the
+  // chains are at most an eighth of the batch (>= kMinCopyChain frames) and each
+  // chain's outputs cross PCIe on the copy stream while the next chains render:
+  // the batch then costs about its copies plus one chain's render, not the sum.
+  constexpr uint32_t kCopyChunks = 8, kMinCopyChain = 32;
+  uint32_t G = c->chain_frames;
+  if (!dev) {
+    G = std::min(G, std::max(kMinCopyChain, (F + kCopyChunks - 1) / kCopyChunks));
+    if (!c->copy_stream) {
+      HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+      for (auto& e : c->copy_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIP_TRY(c, hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming));
+    }
+  }
   HIP_TRY(c, hipMemsetAsync(c->plan_need.p, 0, 2 * sizeof(uint64_t), st));   // k_plan: max over the chains
-  for (uint32_t c0 = 0; c0 < F; c0 += G) {
+  for (uint32_t c0 = 0, chain = 0; c0 < F; c0 += G, ++chain) {
     const uint32_t Fc = std::min(G, F - c0);
     BatchDev bc = b;
     bc.frames = dframes + c0;
@@ -1026,29 +1049,38 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       }
     }
     c->last_F = Fc;
+    if (!dev) {   // this chain's outputs to the host, on the copy stream, behind its kernels
+      hipEvent_t e = c->copy_ev[chain % csg_ctx::kCopyEv];
+      hipStream_t cs = c->copy_stream;
+      HIP_TRY(c, hipEventRecord(e, st));
+      HIP_TRY(c, hipStreamWaitEvent(cs, e, 0));
+      auto copy = [&](void* dst, const void* src, size_t per_frame) -> hipError_t {
+        return hipMemcpyAsync(static_cast<uint8_t*>(dst) + c0 * per_frame,
+                              static_cast<const uint8_t*>(src) + c0 * per_frame, Fc * per_frame,
+                              hipMemcpyDeviceToHost, cs);
+      };
+      if (out->rgb) HIP_TRY(c, copy(out->rgb, b.rgb, npx * 3));
+      if (out->instance) HIP_TRY(c, copy(out->instance, b.inst, npx * 4));
+      if (out->depth) HIP_TRY(c, copy(out->depth, b.depth, npx * 4));
+      if (out->normals) HIP_TRY(c, copy(out->normals, b.normals, npx * 6));
+      if (out->points) HIP_TRY(c, copy(out->points, b.points, npx * 12));
+      if (b.stats) HIP_TRY(c, copy(out->inst_stats, b.stats, (size_t)out->n_labels * 5 * 4));
+      if (b.covered) HIP_TRY(c, copy(out->label_covered, b.covered, (size_t)out->n_labels * 4));
+      if (out->depth_vis) HIP_TRY(c, copy(out->depth_vis, dvis, npx * 3));
+      if (drange_out) HIP_TRY(c, copy(out->depth_range, drange_out, 8));
+      if (dstats) HIP_TRY(c, copy(out->depth_stats, dstats, 48));
+      if (want_kp && out->keypoints_uv) HIP_TRY(c, copy(out->keypoints_uv, b.kp_uv, (size_t)c->n_kp * 8));
+      if (want_kp && out->keypoints_vis) HIP_TRY(c, copy(out->keypoints_vis, b.kp_vis, (size_t)c->n_kp * 4));
+    }
   }
   HIP_TRY(c, hipGetLastError());
   c->last_rgb = b.rgb;
   c->last_depth = b.depth;
   c->last_points = b.points;
   c->last_dvis = dvis;
-  if (!dev) {
-    if (out->rgb) HIP_TRY(c, hipMemcpyAsync(out->rgb, b.rgb, F * npx * 3, hipMemcpyDeviceToHost, st));
-    if (out->instance) HIP_TRY(c, hipMemcpyAsync(out->instance, b.inst, F * npx * 4, hipMemcpyDeviceToHost, st));
-    if (out->depth) HIP_TRY(c, hipMemcpyAsync(out->depth, b.depth, F * npx * 4, hipMemcpyDeviceToHost, st));
-    if (out->normals) HIP_TRY(c, hipMemcpyAsync(out->normals, b.normals, F * npx * 6, hipMemcpyDeviceToHost, st));
-    if (out->points) HIP_TRY(c, hipMemcpyAsync(out->points, b.points, F * npx * 12, hipMemcpyDeviceToHost, st));
-    if (b.stats)
-      HIP_TRY(c, hipMemcpyAsync(out->inst_stats, b.stats, (size_t)F * out->n_labels * 5 * 4, hipMemcpyDeviceToHost, st));
-    if (b.covered)
-      HIP_TRY(c, hipMemcpyAsync(out->label_covered, b.covered, (size_t)F * out->n_labels * 4, hipMemcpyDeviceToHost, st));
-    if (out->depth_vis) HIP_TRY(c, hipMemcpyAsync(out->depth_vis, dvis, F * npx * 3, hipMemcpyDeviceToHost, st));
-    if (drange_out) HIP_TRY(c, hipMemcpyAsync(out->depth_range, drange_out, (size_t)F * 8, hipMemcpyDeviceToHost, st));
-    if (dstats) HIP_TRY(c, hipMemcpyAsync(out->depth_stats, dstats, (size_t)F * 48, hipMemcpyDeviceToHost, st));
-    if (want_kp && out->keypoints_uv)
-      HIP_TRY(c, hipMemcpyAsync(out->keypoints_uv, b.kp_uv, (size_t)F * c->n_kp * 8, hipMemcpyDeviceToHost, st));
-    if (want_kp && out->keypoints_vis)
-      HIP_TRY(c, hipMemcpyAsync(out->keypoints_vis, b.kp_vis, (size_t)F * c->n_kp * 4, hipMemcpyDeviceToHost, st));
+  if (!dev) {   // the batch's stream orders everything after it (and csg_synchronize) behind the copies
+    HIP_TRY(c, hipEventRecord(c->copy_done, c->copy_stream));
+    HIP_TRY(c, hipStreamWaitEvent(st, c->copy_done, 0));
   }
   return CSG_OK;
 }

@@ -943,10 +943,19 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
 // fragments skip the test.  `Small` records (every vertex within 64 px of the
 // tile origin) do the exact arithmetic in 32 bits with full-rate 24-bit
 // multiplies; others in int64.
+// CSG_L1_PRE: a small record's staged groups 0-1 hold its edges' row-
+// independent parts instead of its vertices (stage_record): per edge a -> b
+// base = dy * ax - dx * ay + bias and (dx, dy) as 16-bit halves, so a row's
+// edge value is c0 = dx * cy + base, the same integer as below.
+#ifndef CSG_L1_PRE
+#define CSG_L1_PRE 0
+#endif
 template <bool Small>
-__device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, int ox, int oy, int ly, int x0, int x1,
+__device__ __forceinline__ void row_span(const uint4& g0, const uint4& g1, int ox, int oy, int ly, int x0, int x1,
                                          int& xl, int& xr, bool no_exact) {
   using T = typename std::conditional<Small, int32_t, int64_t>::type;
+  const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
+  const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
   const int32_t OX = ox * 256, OY = oy * 256;
   const int32_t cy = ly * 256 + 128;
   T c0[3];
@@ -955,11 +964,20 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
   const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
-    const int32_t ax = RX[ea[e]] - OX, ay = RY[ea[e]] - OY;
-    const int32_t dx = RX[eb[e]] - RX[ea[e]], dy = RY[eb[e]] - RY[ea[e]];
-    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-    if constexpr (Small) c0[e] = __mul24(dx, cy - ay) + __mul24(dy, ax) + bias;
-    else c0[e] = (int64_t)dx * (cy - ay) + (int64_t)dy * ax + bias;
+    int32_t dy;
+    if constexpr (Small && CSG_L1_PRE) {
+      const uint32_t dd = e == 0 ? g0.w : e == 1 ? g1.x : g1.y;
+      const int32_t dx = (int32_t)(int16_t)(dd & 0xFFFFu);
+      dy = (int32_t)dd >> 16;
+      c0[e] = __mul24(dx, cy) + RX[e];   // RX[e] = base of edge e here
+    } else {
+      const int32_t ax = RX[ea[e]] - OX, ay = RY[ea[e]] - OY;
+      const int32_t dx = RX[eb[e]] - RX[ea[e]];
+      dy = RY[eb[e]] - RY[ea[e]];
+      const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+      if constexpr (Small) c0[e] = __mul24(dx, cy - ay) + __mul24(dy, ax) + bias;
+      else c0[e] = (int64_t)dx * (cy - ay) + (int64_t)dy * ax + bias;
+    }
     dys[e] = dy;
     // boundary of the edge on this row, approximate (rcp: ~2 ulp, far below
     // the 1/16-px margin where it matters); branch-free (no divergence)
@@ -1021,16 +1039,18 @@ __device__ __forceinline__ void row_span(const int32_t* RX, const int32_t* RY, i
 // 256-thread workgroups per CU need <= 22 KiB of LDS each (124 staged 80-B
 // records, 116 shade-table slots) and <= 72 VGPRs.
 // Per tile shape (workgroup size): 124 staged records / 116 shade slots for
-// 256-thread workgroups (32 x 32), 60 / 64 for 128-thread ones (32 x 16);
-// either way 7 waves per SIMD fit the LDS and the 72-VGPR budget.
+// 256-thread workgroups (32 x 32), 64 / 64 for 128-thread ones (32 x 16; 56 /
+// 60 / 64 staged: k_raster 98.6 / 97.0 / 96.2 ms per 2,880 frames, 64 is the
+// most the LDS holds); either way 7 waves per SIMD fit the LDS and the 72-VGPR
+// budget.
 #ifndef CSG_STAGE
-#define CSG_STAGE (kRasterBlock >= 256 ? 124 : 60)
+#define CSG_STAGE (kRasterBlock >= 256 ? 124 : 64)
 #endif
 #ifndef CSG_WAVES
 #define CSG_WAVES 7             // k_raster waves per SIMD to budget registers for
 #endif
 #ifndef CSG_COV_STAGE          // k_raster<true>: smaller batches pay for the coverage table (7 waves per SIMD)
-#define CSG_COV_STAGE (kRasterBlock >= 256 ? 72 : 32)
+#define CSG_COV_STAGE (kRasterBlock >= 256 ? 72 : 38)
 #endif
 #ifndef CSG_COV_WAVES
 #define CSG_COV_WAVES 7
@@ -1216,11 +1236,14 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 #pragma unroll
   for (int k = 0; k < kRecGroups; ++k) q[k] = src[k];
 #pragma unroll
-  for (int k = 0; k < kRecGroups; ++k) img.q[k][slot] = q[k];
+  for (int k = CSG_L1_PRE ? 2 : 0; k < kRecGroups; ++k) img.q[k][slot] = q[k];
   const uint32_t p0 = q[1].z, p1 = q[1].w;            // px0 | py0 << 16, px1 | py1 << 16
   int y0 = max((int)(p0 >> 16), oy), y1 = min((int)(p1 >> 16), oy + kTileH - 1);
   const int x0 = max((int)(p0 & 0xFFFFu), ox), x1 = min((int)(p1 & 0xFFFFu), ox + kTileW - 1);
-  if (x0 > x1 || y0 > y1) return 0u;
+  if (x0 > x1 || y0 > y1) {
+    if (CSG_L1_PRE) { img.q[0][slot] = q[0]; img.q[1][slot] = q[1]; }
+    return 0u;
+  }
   // Rows of the triangle inside this tile's column strip: the y-range of the
   // triangle clipped to the pixel-centre lines x0..x1, in float relative to
   // the tile, widened by half a pixel (>> any rounding here); the exact row
@@ -1251,11 +1274,32 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
       }
     }
   }
-  if (!(ylo <= yhi)) return 0u;
   bool small = true;
 #pragma unroll
   for (int k = 0; k < 3; ++k)
     small &= abs(X[k] - ox * 256) < (1 << 14) && abs(Y[k] - oy * 256) < (1 << 14);
+  if (CSG_L1_PRE) {
+    if (small) {   // row-independent edge parts for level 1 (see row_span)
+      const int32_t OX = ox * 256, OY = oy * 256;
+      const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+      int32_t base[3];
+      uint32_t dd[3];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const int32_t ax = X[ea[e]] - OX, ay = Y[ea[e]] - OY;
+        const int32_t dx = X[eb[e]] - X[ea[e]], dy = Y[eb[e]] - Y[ea[e]];
+        const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+        base[e] = __mul24(dy, ax) - __mul24(dx, ay) + bias;
+        dd[e] = ((uint32_t)dx & 0xFFFFu) | ((uint32_t)dy << 16);
+      }
+      img.q[0][slot] = make_uint4((uint32_t)base[0], (uint32_t)base[1], (uint32_t)base[2], dd[0]);
+      img.q[1][slot] = make_uint4(dd[1], dd[2], p0, p1);
+    } else {
+      img.q[0][slot] = q[0];
+      img.q[1][slot] = q[1];
+    }
+  }
+  if (!(ylo <= yhi)) return 0u;
   // Vertices within 64 px of the tile: every value above is below 2^16 units
   // and off by < 0.01 units, so a 1/16-px widening suffices (half a pixel
   // otherwise added about one empty row per record and tile).
@@ -1340,17 +1384,15 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
         const int k = (int)(cr & 255u);
         const uint32_t first = cr >> 8;
         const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
-        const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
-        const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
         const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTileW - 1);
         const uint32_t r0b = L.row0[k];
         const int ly = (int)(r0b & 31u) + (int)(j1 - first);
         int xr;
         if (DBG(b.dbg) & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
-        else if (r0b & 0x80u) row_span<true>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
+        else if (r0b & 0x80u) row_span<true>(g0, g1, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
         else {
           if (DBG(b.dbg) & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
-          row_span<false>(RX, RY, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
+          row_span<false>(g0, g1, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
         }
         if (xl <= xr) {
           w2 = (uint32_t)(xr - xl + 1);

@@ -172,9 +172,11 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     n_writers = writers or default_writers()
     # Renderer contexts on the device, each with its own stream and work
     # buffers, rendering alternate batches from their own threads: one batch's
-    # encode and copy overlap the next one's render (C3 1080p into RAM, 16
-    # writers: 1,038 frames/s with two, 846 with one).
-    n_rend = renderers or (2 if gpu_files else 1)
+    # encode and copy overlap the next ones' render (C3 1080p into RAM, 16
+    # writers: 1,038 frames/s with two, 846 with one; at steady state with the
+    # files to /dev/null, three: 1,823 / 515 frames/s without / with the point
+    # cloud, two: 1,739 / 505; profiles/r05/generate_steady.json).
+    n_rend = renderers or (3 if gpu_files else 1)
     # the writer processes start here, before this process touches the GPU
     pool = WriterPool(output_spec(batch, wl.height, wl.width, wl.n_keypoints(), scene_labels(wl.scene), want),
                       n_writers, n_slots=2 + n_rend, mode=writer_mode, sink=sink)
@@ -380,7 +382,7 @@ def main(argv=None):
     ap.add_argument("--writers", type=int, default=0, help="writer processes (0: the CPUs this process may use)")
     ap.add_argument("--writer-mode", default="thread", choices=("thread", "process"))
     ap.add_argument("--renderers", type=int, default=0,
-                    help="renderer contexts rendering alternate batches (0: 2 with writer threads, else 1)")
+                    help="renderer contexts rendering alternate batches (0: 3 with writer threads, else 1)")
     ap.add_argument("--object-list", default="visible", choices=OBJECT_LISTS,
                     help="objects in each label file: with visible pixels, or also every one in the view frustum")
     ap.add_argument("--occlusion", action="store_true",
