@@ -187,12 +187,15 @@ struct csg_ctx {
   hipEvent_t* ev = nullptr;             // events of the most recent batch
   uint32_t last_F = 0;
   uint32_t dbg = 0;                     // CSG_DEBUG ablation bits (profiling builds of the pipeline only)
-  // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only).  16 at the
-  // 32 x 16 tiles keeps the [blocks][tiles] count grid the size 32 blocks gave
-  // 32 x 32 tiles (C3 32 x 16: binning 2.27 vs 2.69 ms per 960 frames with 16 vs
-  // 32 blocks; at 2,880 frames per step 8 / 16 / 24 blocks: binning 5.8 / 6.2 /
-  // 6.3 ms, k_raster 97.3 / 97.1 / 96.9 ms; profiles/r05/ab/tile_shape.md)
-  uint32_t bin_blocks = kTileH >= 32 ? 32 : 16;
+  // k_count / k_bin workgroups per frame (CSG_BINBLOCKS: A/B only; set in
+  // csg_create from the tile count).  16 at 1080p's 4,080 tiles of 32 x 16
+  // keeps the [blocks][tiles] count grid the size 32 blocks gave 32 x 32 tiles
+  // (C3: binning 2.27 vs 2.69 ms per 960 frames with 16 vs 32 blocks; at 2,880
+  // frames per step 8 / 16 / 24 blocks: binning 5.8 / 6.2 / 6.3 ms, k_raster
+  // 97.3 / 97.1 / 96.9 ms); 8 above 8,192 tiles (C5 at 4K, 16,200 tiles, 480
+  // frames: binning 4.3 / 4.7 / 4.4 / 5.2 ms with 8 / 16 / 4 / 2 blocks;
+  // profiles/r05/ab/tile_shape.md)
+  uint32_t bin_blocks = 32;
   uint32_t chain_frames = 0;            // frames per launch chain (cfg.frames_per_launch; CSG_CHAIN overrides)
   // Host outputs: each launch chain's slice is copied to the host on copy_stream
   // while the next chains render (created with the first host-output batch).
@@ -292,19 +295,22 @@ const char* csg_last_error(const csg_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int csg_create(const csg_config* cfg, csg_ctx** out) {
   if (!cfg || !out) return CSG_ERR_INVALID;
   *out = nullptr;
-  if (cfg->width == 0 || cfg->height == 0 || cfg->width > 8192 || cfg->height > 8192 || cfg->max_frames == 0 ||
+  // tile rectangles carry 8-bit tile coordinates (k_setup's rect, k_count / k_bin): at most 256 x 256 tiles
+  if (cfg->width == 0 || cfg->height == 0 || cfg->width > 256u * kTileW || cfg->height > 256u * kTileH ||
+      cfg->max_frames == 0 ||
       !(cfg->near_clip >= 0x1p-126f) || !(cfg->far_clip > cfg->near_clip) || !(cfg->far_clip <= 0x1p126f))
     return CSG_ERR_INVALID;   // clip distances in [2^-126, 2^126]: the range of rcp_ieee's proof (k_setup, k_raster)
   csg_ctx* c = new csg_ctx();
   c->cfg = *cfg;
   if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
-  if (const char* v = getenv("CSG_BINBLOCKS")) c->bin_blocks = std::max(1, std::min(1024, atoi(v)));
   c->chain_frames = cfg->frames_per_launch ? cfg->frames_per_launch : kAutoChainFrames;
   if (const char* v = getenv("CSG_CHAIN")) c->chain_frames = (uint32_t)std::max(1, atoi(v));
   c->chain_frames = std::min(c->chain_frames, cfg->max_frames);
   c->tiles_x = (cfg->width + kTileW - 1) / kTileW;
   c->tiles_y = (cfg->height + kTileH - 1) / kTileH;
   c->n_tiles = c->tiles_x * c->tiles_y;
+  c->bin_blocks = kTileH >= 32 ? 32u : (c->n_tiles > 8192u ? 8u : 16u);
+  if (const char* v = getenv("CSG_BINBLOCKS")) c->bin_blocks = std::max(1, std::min(1024, atoi(v)));
   hipError_t e = hipSetDevice(cfg->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   c->ring.assign((size_t)csg_ctx::kRing * 5, nullptr);

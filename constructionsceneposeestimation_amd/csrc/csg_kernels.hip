@@ -46,6 +46,9 @@ namespace csg {
 // code (CSG_STAGE, CSG_WAVES, ...), not alternative paths.
 
 constexpr int kSmallCover = 4;   // records with at most 4 x 4 pixel centres get an exact cover test in k_setup
+#ifndef CSG_COVER_MASK
+#define CSG_COVER_MASK 0          // that test as a 16-bit coverage mask (see make_rec)
+#endif
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr float kGuardPx = 1048576.0f;
 
@@ -421,6 +424,38 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
       nwm += __any(nw >= k) ? 1 : 0;
       nhm += __any(nh >= k) ? 1 : 0;
     }
+#if CSG_COVER_MASK
+    // E(i, j) = e0 + sx*i + sy*j >= 0 as r(j) >= -sx*i with r(j) = e0 + sy*j
+    // stepped per row and the thresholds -sx*i per column precomputed (the same
+    // integers): three compares per centre, whose conjunction is scalar work,
+    // set one bit of a 4x4 coverage mask; the box limits and the row / column
+    // unions are applied to the mask once.
+    int32_t thr[3][N];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      thr[e][0] = 0;
+#pragma unroll
+      for (int i = 1; i < N; ++i) thr[e][i] = thr[e][i - 1] - sx[e];
+    }
+    int32_t er[3] = {e0[0], e0[1], e0[2]};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      if (j > nhm) break;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        if (i > nwm) break;
+        const bool in = er[0] >= thr[0][i] && er[1] >= thr[1][i] && er[2] >= thr[2][i];
+        m |= in ? 1u << (i + N * j) : 0u;
+      }
+#pragma unroll
+      for (int e = 0; e < 3; ++e) er[e] += sy[e];
+    }
+    static_assert(N == 4, "4x4 mask");
+    m &= (((2u << nw) - 1u) * 0x1111u) & ((1u << (4 * nh + 4)) - 1u);   // centres inside the box
+    cols = (m | (m >> 4) | (m >> 8) | (m >> 12)) & 0xFu;
+    rows = ((m & 0xFu) ? 1u : 0u) | ((m & 0xF0u) ? 2u : 0u) | ((m & 0xF00u) ? 4u : 0u) | ((m & 0xF000u) ? 8u : 0u);
+#else
     // E(i, j) = e0 + sx*i + sy*j stepped by additions (the same integers; a
     // constant multiple such as sx*3 otherwise became a quarter-rate v_mul_lo_u32)
     int32_t er[3] = {e0[0], e0[1], e0[2]};
@@ -440,6 +475,7 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
 #pragma unroll
       for (int e = 0; e < 3; ++e) er[e] += sy[e];
     }
+#endif
     if (!cols) return false;
     px1 = px0 + 31 - __clz(cols);
     px0 += __ffs(cols) - 1;

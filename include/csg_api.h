@@ -67,7 +67,8 @@ typedef struct csg_ctx csg_ctx;
 
 typedef struct {
   int32_t device;            /* HIP device ordinal (after HIP_VISIBLE_DEVICES) */
-  uint32_t width, height;    /* output resolution, e.g. 1920x1080 */
+  uint32_t width, height;    /* output resolution, e.g. 1920x1080; at most 8192 x 4096 (256 x 256
+                                tiles of 32 x 16: CSG_ERR_INVALID beyond) */
   uint32_t max_frames;       /* frames per csg_render_batch call (work buffers sized for it) */
   float near_clip, far_clip; /* 0.5 / 250 m, generate_construction_data.py:1437; in [2^-126, 2^126] */
   uint32_t records_per_frame;/* raster-triangle capacity per frame (0 = auto) */

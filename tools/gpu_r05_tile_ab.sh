@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r05/ab
 mkdir -p $O
 L=$PWD/constructionsceneposeestimation_amd
-ARGS="--steps ${STEPS:-8} --warmup 1 --frames-per-step ${FPS:-960} --pcie-steps 0 --stats-steps ${STATS:-0} --cpu-single-frames 1"
+ARGS="--steps ${STEPS:-8} --warmup 1 --frames-per-step ${FPS:-960} --pcie-steps 0 --stats-steps ${STATS:-0} --cpu-single-frames 1 ${EXTRA}"
 # 1. the counters this GPU's profiler offers
 timeout -s KILL 60 rocprofv3 -L > $O/avail.txt 2>&1 || echo "list-avail failed"
 want="SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_ANY SQ_WAVE_CYCLES"
