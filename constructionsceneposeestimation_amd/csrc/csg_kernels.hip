@@ -738,6 +738,14 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
 // ---------------------------------------------------------------------------
 constexpr int kBinRpt = 4;
 constexpr uint32_t kBinRound = kBlock * kBinRpt;
+// k_count / k_bin keep one LDS counter per tile.  A workgroup may hold at most
+// 160 KiB of LDS, so frames of more than kBinBand tiles (16.8 M pixels at
+// 32x16, e.g. 8192 x 2048; the limit is 256 x 256 tiles) are binned in bands
+// of kBinBand tiles:
+// each band re-reads the 4-B tile rectangles and counts / places only the
+// entries of its own tiles.  Below that (every BASELINE workload) there is one
+// band and the kernels run as before.
+constexpr uint32_t kBinBand = 32768;
 
 // last k in [0, kBinRound) with pre[k] <= j (pre: kBinRound + 1 entries,
 // nondecreasing).  4-ary search: each step issues three independent LDS reads,
@@ -805,29 +813,37 @@ __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn_count[];
-  uint32_t* hist = dyn_count;                          // [n_tiles]
-  uint32_t* pre = dyn_count + ((s.n_tiles + 3u) & ~3u);   // [kBinRound + 1]
+  const uint32_t band = min(s.n_tiles, kBinBand);
+  uint32_t* hist = dyn_count;                          // [band]
+  uint32_t* pre = dyn_count + ((band + 3u) & ~3u);     // [kBinRound + 1]
   uint32_t* lrc = pre + kBinRound + 4;                 // [kBinRound]
   uint32_t* wsum = lrc + kBinRound;                    // [4]
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x;
   const uint32_t n = min(b.rec_count[f * kCounterStride], b.slab[f].rec_cap);
   const uint32_t* rect = b.rect + b.slab[f].rec_base;
-  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) hist[t] = 0;
-  __syncthreads();
-  for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-    const uint32_t total = bin_round_setup<kCountDirect>(rect, base, n, lrc, pre, wsum, s.tiles_x,
-                                                 [&](int, uint32_t t) { atomicAdd(&hist[t], 1u); });
-    __syncthreads();
-    for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_bin_item(pre, j);
-      atomicAdd(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
-    }
-    __syncthreads();
-  }
   // this block's row of the count grid (k_colscan turns it into offsets)
   uint32_t* bc = b.bcount + ((size_t)f * gridDim.x + blockIdx.x) * s.n_tiles;
-  for (uint32_t t = tid; t < s.n_tiles; t += kBlock) bc[t] = hist[t];
+  for (uint32_t t0 = 0; t0 < s.n_tiles; t0 += band) {
+    const uint32_t nb = min(band, s.n_tiles - t0);   // tiles [t0, t0 + nb)
+    for (uint32_t t = tid; t < nb; t += kBlock) hist[t] = 0;
+    __syncthreads();
+    for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
+      const uint32_t total = bin_round_setup<kCountDirect>(rect, base, n, lrc, pre, wsum, s.tiles_x,
+                                                   [&](int, uint32_t t) {
+                                                     if (t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
+                                                   });
+      __syncthreads();
+      for (uint32_t j = tid; j < total; j += kBlock) {
+        const int k = find_bin_item(pre, j);
+        const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
+        if (t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
+      }
+      __syncthreads();
+    }
+    for (uint32_t t = tid; t < nb; t += kBlock) bc[t0 + t] = hist[t];
+    __syncthreads();   // (the next band zeroes hist)
+  }
 }
 
 // Column scan of the count grid: per tile, the exclusive prefix over the
@@ -934,7 +950,7 @@ __global__ __launch_bounds__(256) void k_scan(SceneDev s, BatchDev b) {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   extern __shared__ uint32_t dyn[];
-  uint32_t* hist = dyn;                  // [n_tiles] next slot of each tile
+  uint32_t* hist = dyn;                  // [band] next slot of each tile of the band
   __shared__ uint32_t pre[kBinRound + 1];
   __shared__ uint32_t lrc[kBinRound];
   __shared__ uint32_t wsum[kBlock / 64];
@@ -952,18 +968,25 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   // (-0.8% on C3: the scene's small foreground proxies, appended last, reach
   // the z-buffer first).
   const uint32_t* tcnt = b.tile_count + (size_t)f * s.n_tiles;
-  for (uint32_t t = tid; t < s.n_tiles; t += kBlock)
-    hist[t] = toff[t] + tcnt[t] - bo[t] - 1u;   // last slot of the mirrored range; decremented
-  __syncthreads();
-  for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-    const uint32_t total = bin_round_setup<0>(rect, base, n, lrc, pre, wsum, s.tiles_x, [](int, uint32_t) {});
+  const uint32_t band = min(s.n_tiles, kBinBand);
+  for (uint32_t t0 = 0; t0 < s.n_tiles; t0 += band) {
+    const uint32_t nb = min(band, s.n_tiles - t0);   // tiles [t0, t0 + nb)
+    for (uint32_t t = tid; t < nb; t += kBlock)
+      hist[t] = toff[t0 + t] + tcnt[t0 + t] - bo[t0 + t] - 1u;   // last slot of the mirrored range; decremented
     __syncthreads();
-    for (uint32_t j = tid; j < total; j += kBlock) {
-      const int k = find_bin_item(pre, j);
-      const uint32_t slot = atomicSub(&hist[rect_tile(lrc[k], j - pre[k], s.tiles_x)], 1u);
-      if (slot < sb.bin_cap) bins[slot] = base + (uint32_t)k;
+    for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
+      const uint32_t total = bin_round_setup<0>(rect, base, n, lrc, pre, wsum, s.tiles_x, [](int, uint32_t) {});
+      __syncthreads();
+      for (uint32_t j = tid; j < total; j += kBlock) {
+        const int k = find_bin_item(pre, j);
+        const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
+        if (t - t0 < nb) {
+          const uint32_t slot = atomicSub(&hist[t - t0], 1u);
+          if (slot < sb.bin_cap) bins[slot] = base + (uint32_t)k;
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -2330,7 +2353,8 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
 }
 
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
-  const size_t lds = (((s.n_tiles + 3u) & ~3u) + 2 * kBinRound + 12) * sizeof(uint32_t);
+  const uint32_t band = s.n_tiles < kBinBand ? s.n_tiles : kBinBand;
+  const size_t lds = (((band + 3u) & ~3u) + 2 * kBinRound + 12) * sizeof(uint32_t);
   hipLaunchKernelGGL(k_count, dim3(blocks, F), dim3(kBlock), lds, st, s, b);
 }
 
@@ -2346,7 +2370,8 @@ void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t s
 
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
   dim3 g(blocks, F);
-  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), s.n_tiles * sizeof(uint32_t), st, s, b);
+  const uint32_t band = s.n_tiles < kBinBand ? s.n_tiles : kBinBand;
+  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), band * sizeof(uint32_t), st, s, b);
 }
 
 void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {

@@ -1,0 +1,36 @@
+"""The largest frames the library accepts, bit-exact against the oracle.
+
+A raster record's tile rectangle packs tile coordinates in 8 bits
+(`rec_tile_rect`), so `csg_create` accepts at most 256 x 256 tiles of 32x16:
+8192 x 4096 px (`tests/test_abi.py` pins the rejection one pixel beyond).
+Here the limit itself renders: tile coordinate 255 in both axes, 65,536 tiles
+per frame (8 binning blocks per frame above 8,192 tiles), and a one-tile-row
+frame at the full width with a ragged height.  Above 32,768 tiles the binning
+kernels' per-tile LDS counters no longer fit a workgroup's 160 KiB, so they bin
+in bands of tiles (`kBinBand`): 8192 x 4096 takes two full bands, 6000 x 3000
+(188 x 188 ragged tiles) a full band and a short one.  (Round 5: before the
+bands, the 8192 x 4096 launch failed with "invalid argument".)
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import WORLD2_POSES, pose_frames
+from tests.test_gpu_parity import _assert_same, _frames, _oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("W,H", [(8192, 4096), (6000, 3000), (8192, 11)])
+def test_largest_frame(world2, W, H):
+    from constructionsceneposeestimation_amd.renderer import Renderer
+    views, projs = pose_frames(WORLD2_POSES[5:6], W, H)   # a pitched view: geometry to the bottom row
+    ora = _oracle(world2, W, H).render(views[0], projs[0])
+    with Renderer(world2, W, H, max_frames=1) as r:
+        gpu = r.render(_frames(views, projs), want=("rgb", "instance", "depth", "stats"))
+    # geometry reaches the last tile column (and, at full height, the last tile row)
+    inst = ora["instance"]
+    assert (inst[:, -32:] >= 0).any()
+    if H >= 3000:
+        assert (inst[-16:, :] >= 0).any()
+    _assert_same(gpu, ora, 0)
+    assert np.array_equal(gpu["inst_stats"][0], ora["inst_stats"])
