@@ -811,6 +811,7 @@ __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32
 // ---------------------------------------------------------------------------
 // k_count: per-tile record counts (LDS-aggregated, grid-stride over a frame's records)
 // ---------------------------------------------------------------------------
+template <bool kBanded>
 __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn_count[];
   const uint32_t band = min(s.n_tiles, kBinBand);
@@ -831,13 +832,13 @@ __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
     for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
       const uint32_t total = bin_round_setup<kCountDirect>(rect, base, n, lrc, pre, wsum, s.tiles_x,
                                                    [&](int, uint32_t t) {
-                                                     if (t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
+                                                     if (!kBanded || t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
                                                    });
       __syncthreads();
       for (uint32_t j = tid; j < total; j += kBlock) {
         const int k = find_bin_item(pre, j);
         const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
-        if (t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
+        if (!kBanded || t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
       }
       __syncthreads();
     }
@@ -948,6 +949,7 @@ __global__ __launch_bounds__(256) void k_scan(SceneDev s, BatchDev b) {
 // entries of the blocks before it, k_colscan): LDS atomics only, no global
 // atomics, and each block's entries of a tile are a fixed range of its list.
 // ---------------------------------------------------------------------------
+template <bool kBanded>
 __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
   extern __shared__ uint32_t dyn[];
   uint32_t* hist = dyn;                  // [band] next slot of each tile of the band
@@ -980,7 +982,7 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
       for (uint32_t j = tid; j < total; j += kBlock) {
         const int k = find_bin_item(pre, j);
         const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
-        if (t - t0 < nb) {
+        if (!kBanded || t - t0 < nb) {
           const uint32_t slot = atomicSub(&hist[t - t0], 1u);
           if (slot < sb.bin_cap) bins[slot] = base + (uint32_t)k;
         }
@@ -2355,7 +2357,9 @@ void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uin
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
   const uint32_t band = s.n_tiles < kBinBand ? s.n_tiles : kBinBand;
   const size_t lds = (((band + 3u) & ~3u) + 2 * kBinRound + 12) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_count, dim3(blocks, F), dim3(kBlock), lds, st, s, b);
+  // (one band: the kernels without the per-entry band test)
+  if (s.n_tiles > kBinBand) hipLaunchKernelGGL(k_count<true>, dim3(blocks, F), dim3(kBlock), lds, st, s, b);
+  else hipLaunchKernelGGL(k_count<false>, dim3(blocks, F), dim3(kBlock), lds, st, s, b);
 }
 
 void launch_plan(const FrameDev* frames, uint32_t F, uint32_t def_rec, uint32_t def_bin, uint64_t rec_pool,
@@ -2371,7 +2375,8 @@ void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t s
 void launch_bin(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st) {
   dim3 g(blocks, F);
   const uint32_t band = s.n_tiles < kBinBand ? s.n_tiles : kBinBand;
-  hipLaunchKernelGGL(k_bin, g, dim3(kBlock), band * sizeof(uint32_t), st, s, b);
+  if (s.n_tiles > kBinBand) hipLaunchKernelGGL(k_bin<true>, g, dim3(kBlock), band * sizeof(uint32_t), st, s, b);
+  else hipLaunchKernelGGL(k_bin<false>, g, dim3(kBlock), band * sizeof(uint32_t), st, s, b);
 }
 
 void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st) {
