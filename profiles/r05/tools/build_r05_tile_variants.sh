@@ -1,5 +1,5 @@
 #!/bin/bash
-# CPU side of tools/gpu_r05_tile_ab.sh: the tile-shape variants of libcsg.so
+# CPU side of tools/gpu_variant_ab.sh: the tile-shape variants of libcsg.so
 # (working-tree kernels; LDS per workgroup sized for 7 waves per SIMD) and
 # their ablation / profiling-counter builds.
 set -e

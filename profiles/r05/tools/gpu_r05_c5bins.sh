@@ -4,4 +4,4 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 REPS=${REPS:-2} STEPS=4 FPS=480 SKIP_LDS=1 CTR_VARIANTS="" EXTRA="--workload C5 --verify-frames 4" \
-  VARIANTS="base:CSG_BINBLOCKS=16 base:CSG_BINBLOCKS=8 base:CSG_BINBLOCKS=4 base:CSG_BINBLOCKS=2" bash tools/gpu_r05_tile_ab.sh
+  VARIANTS="base:CSG_BINBLOCKS=16 base:CSG_BINBLOCKS=8 base:CSG_BINBLOCKS=4 base:CSG_BINBLOCKS=2" bash tools/gpu_variant_ab.sh

@@ -3,7 +3,7 @@
 # the per-phase VALU split of the ablation build (tools/gpu_ablate_valu.sh).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TEST=1 BENCH=1 PROF=${PROF:-0} WORKLOADS="" bash tools/gpu_r05_final.sh || exit 1
+TEST=1 BENCH=1 PROF=${PROF:-0} WORKLOADS="" bash tools/gpu_final.sh || exit 1
 if [ "${ABL:-1}" = 1 ]; then
   bash tools/gpu_ablate_valu.sh || exit 1
 fi

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-REPS=${REPS:-2} STEPS=6 FPS=2880 STATS=2 SKIP_LDS=1 CTR_VARIANTS="" VARIANTS="${VARIANTS:-base ns64 ns56}" bash tools/gpu_r05_tile_ab.sh || exit 1
+REPS=${REPS:-2} STEPS=6 FPS=2880 STATS=2 SKIP_LDS=1 CTR_VARIANTS="" VARIANTS="${VARIANTS:-base ns64 ns56}" bash tools/gpu_variant_ab.sh || exit 1
 O=gpurun_out/r05/gen
 mkdir -p $O
 for R in 3; do

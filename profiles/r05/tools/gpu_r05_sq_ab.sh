@@ -5,4 +5,4 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 REPS=${REPS:-2} STEPS=6 FPS=2880 SKIP_LDS=1 CTR_VARIANTS="" VARIANTS="${VARIANTS:-base sq24 sq14 sq12 sq44}" \
-  bash tools/gpu_r05_tile_ab.sh
+  bash tools/gpu_variant_ab.sh

@@ -7,4 +7,4 @@ O=gpurun_out/r05
 mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_lds_order.py tests/test_gpu_keypoint_sky.py tests/test_gpu_occlusion_depthvis.py tests/test_gpu_headline.py > $O/pytest_swz.log 2>&1 || { tail -30 $O/pytest_swz.log; exit 1; }
 tail -2 $O/pytest_swz.log
-REPS=${REPS:-3} VARIANTS="${VARIANTS:-base noswz w32h16 w32h16_noswz w32h16:CSG_BINBLOCKS=16}" CTR_VARIANTS="" DBGS="${DBGS:-0 1 8}" LDS_TAG=_swz bash tools/gpu_r05_tile_ab.sh
+REPS=${REPS:-3} VARIANTS="${VARIANTS:-base noswz w32h16 w32h16_noswz w32h16:CSG_BINBLOCKS=16}" CTR_VARIANTS="" DBGS="${DBGS:-0 1 8}" LDS_TAG=_swz bash tools/gpu_variant_ab.sh

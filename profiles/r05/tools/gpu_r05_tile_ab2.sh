@@ -6,4 +6,4 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 REPS=${REPS:-2} STEPS=6 FPS=2880 SKIP_LDS=1 CTR_VARIANTS="" \
   VARIANTS="${VARIANTS:-base w32h16:CSG_BINBLOCKS=16 w32h16w6:CSG_BINBLOCKS=16 w32h16:CSG_BINBLOCKS=8 w32h16:CSG_BINBLOCKS=24}" \
-  bash tools/gpu_r05_tile_ab.sh
+  bash tools/gpu_variant_ab.sh

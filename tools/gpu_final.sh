@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 5 (end): GPU suite + smoke, the default bench line, its kernel-trace
+# End of a round: GPU suite + smoke, the default bench line, its kernel-trace
 # profile, the PMC passes (HBM traffic, VALU, LDS) at the default launch size,
 # the driver's exact command, and the other workloads' lines.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r05/final
+O=${OUT:-gpurun_out/final}
 mkdir -p $O
 export TMPDIR=/tmp
 if [ "${TEST:-1}" = 1 ]; then
@@ -24,7 +24,7 @@ if [ "${PROF:-1}" = 1 ]; then
   python3 tools/kernel_stats_by_grid.py $(ls $O/prof/*/kt_kernel_trace.csv $O/prof/kt_kernel_trace.csv 2>/dev/null | head -1) | tee $O/kernel_stats_by_grid.txt
 fi
 if [ -n "$PMC" ]; then
-  ROUND=r05f PASSES="$PMC" bash tools/pmc_profile.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
+  ROUND=${ROUND:-final} PASSES="$PMC" bash tools/pmc_profile.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
   tail -3 $O/pmc.log
 fi
 for w in ${WORKLOADS-C2 C4 C5}; do

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: k_raster's HBM-side traffic split per phase.  The ablation build
+# k_raster's HBM-side traffic split per phase.  The ablation build
 # (libcsg_abl.so: `tools/build_variant.sh abl - -DCSG_ABLATION=1`) with the
 # CSG_DEBUG bits of DESIGN §5 (0 all, 1 no resolve, 8 no level-2 fragments,
 # 256 no level 1, 2 empty-tile resolve only); per setting three rocprofv3
@@ -10,7 +10,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 export CSG_LIB=$PWD/constructionsceneposeestimation_amd/libcsg_abl.so
-OUT=gpurun_out/r05/traffic
+OUT=${OUT:-gpurun_out/traffic}
 mkdir -p $OUT
 ARGS="--steps 3 --warmup 1 --frames-per-step ${FPS:-960} --verify-frames 0 --pcie-steps 0 --stats-steps 0"
 rc=0

@@ -1,12 +1,16 @@
 #!/bin/bash
-# Round 5: k_raster's LDS counters, per phase (ablation build, CSG_DEBUG bits),
-# and the tile-shape A/B (32x32 production vs 64x16 / 32x16 / 16x16 and a
-# 32x32 control with the 64x16 build's smaller batches).  Libraries are built
-# on the CPU beforehand (tools/build_r05_tile_variants.sh).
+# A/B of library variants on bench.py (round 5's tile-shape driver, now the
+# generic one): VARIANTS="base name[:ENV=val]..." runs libcsg.so ("base") and
+# libcsg_<name>.so (built on the CPU beforehand by tools/build_variant.sh) REPS
+# times in turn, each line self-verified on 8 frames; optionally the profiling
+# counters per variant (CTR_VARIANTS, CSG_DEBUG=512 builds) and the LDS
+# counters per ablation setting (libcsg_abl.so; SKIP_LDS=1 skips them).
+# Results: $OUT/tile_ab.txt (default gpurun_out/r05/ab, where round 5's
+# scripts under profiles/r05/tools expect them).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r05/ab
+O=${OUT:-gpurun_out/r05/ab}
 mkdir -p $O
 L=$PWD/constructionsceneposeestimation_amd
 ARGS="--steps ${STEPS:-8} --warmup 1 --frames-per-step ${FPS:-960} --pcie-steps 0 --stats-steps ${STATS:-0} --cpu-single-frames 1 ${EXTRA}"
