@@ -1662,6 +1662,10 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
   rgb_out = o;
 }
 
+#ifndef CSG_VEC_OUT
+#define CSG_VEC_OUT 1      // vector stores of the per-pixel outputs (see the resolve)
+#endif
+
 // Resolve-phase LDS (aliases the raster loop's): the tile's distinct winning
 // triangles in an open-addressing table of kShadeSlots, each set up once by
 // one thread, then read by every pixel that shows it.
@@ -2046,12 +2050,26 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
           atomicMax(&st[4], (uint32_t)qy);
         }
       };
+      // The optional per-pixel outputs (depth, normals, points) of a group
+      // whose 4 pixels all lie in the frame and are all finished in this round
+      // go out after the loop as one 16-B depth, three 8-B normal and three
+      // 16-B point stores (lane-contiguous); otherwise, and with CSG_VEC_OUT 0,
+      // each pixel stores its own (4-B, 2-B and 4-B stores at 16-, 6- and 12-B
+      // pixel strides: at 4K those narrow stores were 30% of k_raster).
+      // (o % 4 == 0 keeps the group's outputs 16-B aligned, as in empty_tile.)
+      bool vec = false;
+      if (CSG_VEC_OUT && (b.depth || b.normals || b.points) && inmask == 0xFu && (qo & 3u) == 0) {
+        uint32_t done = first ? bgmask : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) done |= ((slots >> (8 * k)) & 0xFFu) != 0xFFu ? 1u << k : 0u;
+        vec = done == 0xFu;
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int px = qx0 + k;
         const uint32_t sl = (slots >> (8 * k)) & 0xFFu;
         // background pixels are written in the first round; the optional
-        // outputs are stored per pixel so their values are never live long
+        // outputs of a pixel not in a vector group are stored per pixel
         const bool bg = first && ((bgmask >> k) & 1u);
         if (sl == 0xFFu && !bg) continue;
         float dep = INFINITY;
@@ -2076,6 +2094,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
             xmax = (uint32_t)px;
           }
         }
+        if (vec) continue;
         if (b.depth) b.depth[qo + k] = dep;
         if (b.normals) {
           uint16_t* d = b.normals + (qo + k) * 3;
@@ -2094,6 +2113,45 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
         }
       }
       flush_run();
+      if (vec) {   // background pixels (first round): depth +inf, normal 0, point NaN
+        // the depths again, from the table (as shade_pixel: the same bits), so
+        // that none is live across the shading loop
+        const uint32_t bgv = first ? bgmask : 0u;
+        float dv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const ShadeEntry& e = L.q.tab[(bgv >> k) & 1u ? 0u : (slots >> (8 * k)) & 0xFFu];
+          const float fx = (float)(qx0 + k) + 0.5f, fy = (float)qy + 0.5f;
+          dv[k] = ((bgv >> k) & 1u) || !need_depth ? INFINITY : rcp_ieee(plane_at(e.P[0], e.P[1], e.P[2], fx, fy));
+        }
+        if (b.depth) *reinterpret_cast<float4*>(b.depth + qo) = make_float4(dv[0], dv[1], dv[2], dv[3]);
+        if (b.normals) {   // 12 halves x0 y0 z0 x1 ... z3 as 6 words
+          uint32_t n01[4], n2[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool bg = (bgv >> k) & 1u;
+            const ShadeEntry& e = L.q.tab[bg ? 0u : (slots >> (8 * k)) & 0xFFu];
+            n01[k] = bg ? 0u : e.n01;
+            n2[k] = bg ? 0u : e.n2;
+          }
+          uint2* d = reinterpret_cast<uint2*>(b.normals + qo * 3);
+          d[0] = make_uint2(n01[0], n2[0] | (n01[1] << 16));
+          d[1] = make_uint2((n01[1] >> 16) | (n2[1] << 16), n01[2]);
+          d[2] = make_uint2(n2[2] | (n01[3] << 16), (n01[3] >> 16) | (n2[3] << 16));
+        }
+        if (b.points) {
+          float pt[12];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if ((bgv >> k) & 1u) pt[3 * k] = pt[3 * k + 1] = pt[3 * k + 2] = __builtin_nanf("");
+            else unproject(b.cam + (size_t)f * kCamFloats, qx0 + k, qy, dv[k], pt + 3 * k);
+          }
+          float4* d = reinterpret_cast<float4*>(b.points + qo * 3);
+          d[0] = make_float4(pt[0], pt[1], pt[2], pt[3]);
+          d[1] = make_float4(pt[4], pt[5], pt[6], pt[7]);
+          d[2] = make_float4(pt[8], pt[9], pt[10], pt[11]);
+        }
+      }
     }
     if (pend) L.q.more = 1;          // (__syncthreads_or measured 16% slower here)
     __syncthreads();
