@@ -1760,8 +1760,33 @@ __device__ __forceinline__ void out_ids(int32_t* p, int4 v) {
   const v4i32 w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, reinterpret_cast<v4i32*>(p));
 }
+// The optional per-pixel outputs as 16-B / 8-B vector stores, non-temporal
+// as the instance ids (CSG_NT_OUT; outputs are written once and never read
+// back, so they need not displace records and texels from L2: C5 k_raster
+// 66.4 -> 62.2 ms per 480 frames, profiles/r05/ab/tile_shape.md §10).
+#ifndef CSG_NT_OUT
+#define CSG_NT_OUT 1
+#endif
+#ifndef CSG_NT_RGB
+#define CSG_NT_RGB 0
+#endif
+typedef uint32_t v3u32 __attribute__((ext_vector_type(3)));
+typedef float v4f32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void out_f4(float* p, float a, float b2, float c, float d) {
+  const v4f32 w = {a, b2, c, d};
+  if (CSG_NT_OUT) __builtin_nontemporal_store(w, reinterpret_cast<v4f32*>(p));
+  else *reinterpret_cast<v4f32*>(p) = w;
+}
+__device__ __forceinline__ void out_u2(uint16_t* p, uint32_t a, uint32_t b2) {
+  const v2u32 w = {a, b2};
+  if (CSG_NT_OUT) __builtin_nontemporal_store(w, reinterpret_cast<v2u32*>(p));
+  else *reinterpret_cast<v2u32*>(p) = w;
+}
 __device__ __forceinline__ void out_rgb4(uint8_t* p, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-  *reinterpret_cast<uint3*>(p) = make_uint3(c0 | (c1 << 24), (c1 >> 8) | (c2 << 16), (c2 >> 16) | (c3 << 8));
+  const v3u32 w = {c0 | (c1 << 24), (c1 >> 8) | (c2 << 16), (c2 >> 16) | (c3 << 8)};
+  if (CSG_NT_RGB) __builtin_nontemporal_store(w, reinterpret_cast<v3u32*>(p));
+  else *reinterpret_cast<v3u32*>(p) = w;
 }
 
 // A tile without bin entries: every pixel is background (sky, id -1, depth
@@ -1788,14 +1813,12 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
   if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
     if (b.inst) out_ids(b.inst + o, make_int4(-1, -1, -1, -1));
     if (b.rgb) out_rgb4(b.rgb + o * 3, sky, sky, sky, sky);
-    if (b.depth) *reinterpret_cast<float4*>(b.depth + o) = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
+    if (b.depth) out_f4(b.depth + o, INFINITY, INFINITY, INFINITY, INFINITY);
     if (b.normals) {
-      uint2* d = reinterpret_cast<uint2*>(b.normals + o * 3);
-      d[0] = d[1] = d[2] = make_uint2(0u, 0u);
+      for (int w = 0; w < 3; ++w) out_u2(b.normals + o * 3 + 4 * w, 0u, 0u);
     }
     if (b.points) {
-      float4* d = reinterpret_cast<float4*>(b.points + o * 3);
-      d[0] = d[1] = d[2] = make_float4(nan, nan, nan, nan);
+      for (int w = 0; w < 3; ++w) out_f4(b.points + o * 3 + 4 * w, nan, nan, nan, nan);
     }
   } else {
     for (int k = 0; k < 4 && px0 + k < (int)s.W; ++k) {
@@ -2124,7 +2147,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
           const float fx = (float)(qx0 + k) + 0.5f, fy = (float)qy + 0.5f;
           dv[k] = ((bgv >> k) & 1u) || !need_depth ? INFINITY : rcp_ieee(plane_at(e.P[0], e.P[1], e.P[2], fx, fy));
         }
-        if (b.depth) *reinterpret_cast<float4*>(b.depth + qo) = make_float4(dv[0], dv[1], dv[2], dv[3]);
+        if (b.depth) out_f4(b.depth + qo, dv[0], dv[1], dv[2], dv[3]);
         if (b.normals) {   // 12 halves x0 y0 z0 x1 ... z3 as 6 words
           uint32_t n01[4], n2[4];
 #pragma unroll
@@ -2134,10 +2157,10 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
             n01[k] = bg ? 0u : e.n01;
             n2[k] = bg ? 0u : e.n2;
           }
-          uint2* d = reinterpret_cast<uint2*>(b.normals + qo * 3);
-          d[0] = make_uint2(n01[0], n2[0] | (n01[1] << 16));
-          d[1] = make_uint2((n01[1] >> 16) | (n2[1] << 16), n01[2]);
-          d[2] = make_uint2(n2[2] | (n01[3] << 16), (n01[3] >> 16) | (n2[3] << 16));
+          uint16_t* d = b.normals + qo * 3;
+          out_u2(d, n01[0], n2[0] | (n01[1] << 16));
+          out_u2(d + 4, (n01[1] >> 16) | (n2[1] << 16), n01[2]);
+          out_u2(d + 8, n2[2] | (n01[3] << 16), (n01[3] >> 16) | (n2[3] << 16));
         }
         if (b.points) {
           float pt[12];
@@ -2146,10 +2169,10 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
             if ((bgv >> k) & 1u) pt[3 * k] = pt[3 * k + 1] = pt[3 * k + 2] = __builtin_nanf("");
             else unproject(b.cam + (size_t)f * kCamFloats, qx0 + k, qy, dv[k], pt + 3 * k);
           }
-          float4* d = reinterpret_cast<float4*>(b.points + qo * 3);
-          d[0] = make_float4(pt[0], pt[1], pt[2], pt[3]);
-          d[1] = make_float4(pt[4], pt[5], pt[6], pt[7]);
-          d[2] = make_float4(pt[8], pt[9], pt[10], pt[11]);
+          float* d = b.points + qo * 3;
+          out_f4(d, pt[0], pt[1], pt[2], pt[3]);
+          out_f4(d + 4, pt[4], pt[5], pt[6], pt[7]);
+          out_f4(d + 8, pt[8], pt[9], pt[10], pt[11]);
         }
       }
     }
