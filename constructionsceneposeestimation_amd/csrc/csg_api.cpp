@@ -850,6 +850,13 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   c->last_stream = st;
   int rc = sync_scene_state(c);
   if (rc) return rc;
+  if (out->on_device) {   // k_raster writes 4-pixel groups as vector stores (16-B ids, depth, points; 8-B normals)
+    auto mis = [](const void* p, uintptr_t a) { return p && ((uintptr_t)p & (a - 1)) != 0; };
+    if (mis(out->instance, 16) || mis(out->depth, 16) || mis(out->points, 16) || mis(out->normals, 8) ||
+        mis(out->rgb, 4))
+      return c->fail(CSG_ERR_INVALID, "render: device outputs must be aligned (instance, depth, points 16 B; "
+                                      "normals 8 B; rgb 4 B)");
+  }
   rc = ensure_work(c);
   if (rc) return rc;
   const size_t npx = (size_t)c->cfg.width * c->cfg.height;

@@ -128,7 +128,9 @@ typedef struct {
   int32_t* keypoints_vis;    /* [n][K] 0 out/behind, 1 occluded, 2 visible */
   uint32_t* inst_stats;      /* [n][n_labels][5] = pixels, minx, miny, maxx, maxy */
   uint32_t n_labels;
-  int32_t on_device;         /* 1: device pointers (stay in HBM), 0: host pointers */
+  int32_t on_device;         /* 1: device pointers (stay in HBM; instance, depth and points
+                                16-B aligned, normals 8 B, rgb 4 B: CSG_ERR_INVALID otherwise,
+                                as k_raster stores 4-pixel groups), 0: host pointers */
   uint16_t* normals;         /* [n][H][W][3] f16 bits: unit world-space face normal facing
                                 the camera; 0 where nothing is hit (C5 normals) */
   float* points;             /* [n][H][W][3] world-space point of each pixel from its depth
