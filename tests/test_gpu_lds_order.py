@@ -69,13 +69,15 @@ def test_multi_round_resolve_stats_range_coverage_keypoints():
     o = Oracle(pack_scene(sc), W, H)
     refs = []
     for k in range(F):
-        ref = o.render(views[k], projs[k], want_stats=True, covered=True)
+        ref = o.render(views[k], projs[k], want_stats=True, covered=True, extra=True)
         ref["uv"], ref["vis"] = o.keypoints(views[k], projs[k], kp, ref["depth"])
         ref["dvis"], ref["drange"] = depth_vis(ref["depth"])
         refs.append(ref)
     assert len(np.unique(refs[0]["instance"])) >= 40
     assert (refs[0]["vis"] == 2).sum() > 50 and (refs[0]["vis"] == 1).sum() > 50
-    want = ("rgb", "instance", "depth", "stats", "keypoints", "depth_vis")
+    # normals and points too: a 4-pixel group whose pixels finish in different
+    # rounds stores them per pixel, one finished in a single round as vector stores
+    want = ("rgb", "instance", "depth", "stats", "keypoints", "depth_vis", "normals", "points")
     with Renderer(sc, W, H, max_frames=F) as r:
         r.set_keypoints(0, kp)
         for cov in (False, True, False, True, False, True):
@@ -84,6 +86,8 @@ def test_multi_round_resolve_stats_range_coverage_keypoints():
                 for key in ("rgb", "instance"):
                     assert np.array_equal(gpu[key][k], ref[key]), f"frame {k}: {key}"
                 assert np.array_equal(gpu["depth"][k].view(np.uint32), ref["depth"].view(np.uint32)), f"frame {k}"
+                assert np.array_equal(gpu["normals"][k].view(np.uint16), ref["normals"].view(np.uint16)), f"frame {k}"
+                assert np.array_equal(gpu["points"][k].view(np.uint32), ref["points"].view(np.uint32)), f"frame {k}"
                 assert np.array_equal(gpu["inst_stats"][k], ref["inst_stats"]), f"frame {k}: label stats"
                 if cov:
                     assert np.array_equal(gpu["label_covered"][k], ref["label_covered"]), f"frame {k}: coverage"
