@@ -46,9 +46,6 @@ namespace csg {
 // code (CSG_STAGE, CSG_WAVES, ...), not alternative paths.
 
 constexpr int kSmallCover = 4;   // records with at most 4 x 4 pixel centres get an exact cover test in k_setup
-#ifndef CSG_COVER_MASK
-#define CSG_COVER_MASK 0          // that test as a 16-bit coverage mask (see make_rec)
-#endif
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr float kGuardPx = 1048576.0f;
 
@@ -424,38 +421,6 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
       nwm += __any(nw >= k) ? 1 : 0;
       nhm += __any(nh >= k) ? 1 : 0;
     }
-#if CSG_COVER_MASK
-    // E(i, j) = e0 + sx*i + sy*j >= 0 as r(j) >= -sx*i with r(j) = e0 + sy*j
-    // stepped per row and the thresholds -sx*i per column precomputed (the same
-    // integers): three compares per centre, whose conjunction is scalar work,
-    // set one bit of a 4x4 coverage mask; the box limits and the row / column
-    // unions are applied to the mask once.
-    int32_t thr[3][N];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      thr[e][0] = 0;
-#pragma unroll
-      for (int i = 1; i < N; ++i) thr[e][i] = thr[e][i - 1] - sx[e];
-    }
-    int32_t er[3] = {e0[0], e0[1], e0[2]};
-    uint32_t m = 0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      if (j > nhm) break;
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        if (i > nwm) break;
-        const bool in = er[0] >= thr[0][i] && er[1] >= thr[1][i] && er[2] >= thr[2][i];
-        m |= in ? 1u << (i + N * j) : 0u;
-      }
-#pragma unroll
-      for (int e = 0; e < 3; ++e) er[e] += sy[e];
-    }
-    static_assert(N == 4, "4x4 mask");
-    m &= (((2u << nw) - 1u) * 0x1111u) & ((1u << (4 * nh + 4)) - 1u);   // centres inside the box
-    cols = (m | (m >> 4) | (m >> 8) | (m >> 12)) & 0xFu;
-    rows = ((m & 0xFu) ? 1u : 0u) | ((m & 0xF0u) ? 2u : 0u) | ((m & 0xF00u) ? 4u : 0u) | ((m & 0xF000u) ? 8u : 0u);
-#else
     // E(i, j) = e0 + sx*i + sy*j stepped by additions (the same integers; a
     // constant multiple such as sx*3 otherwise became a quarter-rate v_mul_lo_u32)
     int32_t er[3] = {e0[0], e0[1], e0[2]};
@@ -475,7 +440,6 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
 #pragma unroll
       for (int e = 0; e < 3; ++e) er[e] += sy[e];
     }
-#endif
     if (!cols) return false;
     px1 = px0 + 31 - __clz(cols);
     px0 += __ffs(cols) - 1;
@@ -1004,13 +968,6 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
 // fragments skip the test.  `Small` records (every vertex within 64 px of the
 // tile origin) do the exact arithmetic in 32 bits with full-rate 24-bit
 // multiplies; others in int64.
-// CSG_L1_PRE: a small record's staged groups 0-1 hold its edges' row-
-// independent parts instead of its vertices (stage_record): per edge a -> b
-// base = dy * ax - dx * ay + bias and (dx, dy) as 16-bit halves, so a row's
-// edge value is c0 = dx * cy + base, the same integer as below.
-#ifndef CSG_L1_PRE
-#define CSG_L1_PRE 0
-#endif
 template <bool Small>
 __device__ __forceinline__ void row_span(const uint4& g0, const uint4& g1, int ox, int oy, int ly, int x0, int x1,
                                          int& xl, int& xr, bool no_exact) {
@@ -1025,20 +982,12 @@ __device__ __forceinline__ void row_span(const uint4& g0, const uint4& g1, int o
   const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
-    int32_t dy;
-    if constexpr (Small && CSG_L1_PRE) {
-      const uint32_t dd = e == 0 ? g0.w : e == 1 ? g1.x : g1.y;
-      const int32_t dx = (int32_t)(int16_t)(dd & 0xFFFFu);
-      dy = (int32_t)dd >> 16;
-      c0[e] = __mul24(dx, cy) + RX[e];   // RX[e] = base of edge e here
-    } else {
-      const int32_t ax = RX[ea[e]] - OX, ay = RY[ea[e]] - OY;
-      const int32_t dx = RX[eb[e]] - RX[ea[e]];
-      dy = RY[eb[e]] - RY[ea[e]];
-      const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-      if constexpr (Small) c0[e] = __mul24(dx, cy - ay) + __mul24(dy, ax) + bias;
-      else c0[e] = (int64_t)dx * (cy - ay) + (int64_t)dy * ax + bias;
-    }
+    const int32_t ax = RX[ea[e]] - OX, ay = RY[ea[e]] - OY;
+    const int32_t dx = RX[eb[e]] - RX[ea[e]];
+    const int32_t dy = RY[eb[e]] - RY[ea[e]];
+    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+    if constexpr (Small) c0[e] = __mul24(dx, cy - ay) + __mul24(dy, ax) + bias;
+    else c0[e] = (int64_t)dx * (cy - ay) + (int64_t)dy * ax + bias;
     dys[e] = dy;
     // boundary of the edge on this row, approximate (rcp: ~2 ulp, far below
     // the 1/16-px margin where it matters); branch-free (no divergence)
@@ -1297,14 +1246,11 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 #pragma unroll
   for (int k = 0; k < kRecGroups; ++k) q[k] = src[k];
 #pragma unroll
-  for (int k = CSG_L1_PRE ? 2 : 0; k < kRecGroups; ++k) img.q[k][slot] = q[k];
+  for (int k = 0; k < kRecGroups; ++k) img.q[k][slot] = q[k];
   const uint32_t p0 = q[1].z, p1 = q[1].w;            // px0 | py0 << 16, px1 | py1 << 16
   int y0 = max((int)(p0 >> 16), oy), y1 = min((int)(p1 >> 16), oy + kTileH - 1);
   const int x0 = max((int)(p0 & 0xFFFFu), ox), x1 = min((int)(p1 & 0xFFFFu), ox + kTileW - 1);
-  if (x0 > x1 || y0 > y1) {
-    if (CSG_L1_PRE) { img.q[0][slot] = q[0]; img.q[1][slot] = q[1]; }
-    return 0u;
-  }
+  if (x0 > x1 || y0 > y1) return 0u;
   // Rows of the triangle inside this tile's column strip: the y-range of the
   // triangle clipped to the pixel-centre lines x0..x1, in float relative to
   // the tile, widened by half a pixel (>> any rounding here); the exact row
@@ -1339,27 +1285,6 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
 #pragma unroll
   for (int k = 0; k < 3; ++k)
     small &= abs(X[k] - ox * 256) < (1 << 14) && abs(Y[k] - oy * 256) < (1 << 14);
-  if (CSG_L1_PRE) {
-    if (small) {   // row-independent edge parts for level 1 (see row_span)
-      const int32_t OX = ox * 256, OY = oy * 256;
-      const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
-      int32_t base[3];
-      uint32_t dd[3];
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int32_t ax = X[ea[e]] - OX, ay = Y[ea[e]] - OY;
-        const int32_t dx = X[eb[e]] - X[ea[e]], dy = Y[eb[e]] - Y[ea[e]];
-        const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-        base[e] = __mul24(dy, ax) - __mul24(dx, ay) + bias;
-        dd[e] = ((uint32_t)dx & 0xFFFFu) | ((uint32_t)dy << 16);
-      }
-      img.q[0][slot] = make_uint4((uint32_t)base[0], (uint32_t)base[1], (uint32_t)base[2], dd[0]);
-      img.q[1][slot] = make_uint4(dd[1], dd[2], p0, p1);
-    } else {
-      img.q[0][slot] = q[0];
-      img.q[1][slot] = q[1];
-    }
-  }
   if (!(ylo <= yhi)) return 0u;
   // Vertices within 64 px of the tile: every value above is below 2^16 units
   // and off by < 0.01 units, so a 1/16-px widening suffices (half a pixel
