@@ -1693,7 +1693,7 @@ __device__ __forceinline__ void out_ids(int32_t* p, int4 v) {
 #define CSG_NT_OUT 1
 #endif
 #ifndef CSG_NT_RGB
-#define CSG_NT_RGB 0
+#define CSG_NT_RGB 1      // the RGB group stores too (C3 k_raster 96.25 -> 95.86 ms, tile_shape.md §10)
 #endif
 typedef uint32_t v3u32 __attribute__((ext_vector_type(3)));
 typedef float v4f32 __attribute__((ext_vector_type(4)));
