@@ -1590,6 +1590,9 @@ __device__ __forceinline__ void shade_pixel(const SceneDev& s, const ShadeEntry&
 #ifndef CSG_VEC_OUT
 #define CSG_VEC_OUT 1      // vector stores of the per-pixel outputs (see the resolve)
 #endif
+#ifndef CSG_VEC_DEP_ONCE
+#define CSG_VEC_DEP_ONCE 1 // a vector group's shading loop skips the depth (C5 k_raster -0.3%)
+#endif
 
 // Resolve-phase LDS (aliases the raster loop's): the tile's distinct winning
 // triangles in an open-addressing table of kShadeSlots, each set up once by
@@ -2026,7 +2029,8 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
           const ShadeEntry& e = L.q.tab[sl];
           uint32_t rgb;
           int32_t id;
-          shade_pixel(s, e, px, qy, need_depth, rgb, id, dep);
+          // (a vector group's depths are evaluated again after the loop)
+          shade_pixel(s, e, px, qy, need_depth && !(CSG_VEC_DEP_ONCE && vec), rgb, id, dep);
           n01 = e.n01;
           n2 = e.n2;
           zpix(k) = (unsigned long long)rgb | ((unsigned long long)(uint32_t)id << 32);
