@@ -64,6 +64,9 @@ DEFAULT_STEPS, DEFAULT_WARMUP, DEFAULT_FRAMES_PER_STEP = 10, 2, 2880
 # frames/s): ~115 GB of outputs and ~16 GB of work per rank.
 LARGE_FRAME_PIXELS, LARGE_FRAMES_PER_STEP = 1920 * 1080, 480
 MAX_SETS = 65536   # transform sets per context (kMaxSets, csg_api.cpp)
+# Host-delivery batches at N > 1 (every rank at once): 480 frames of C3 are
+# ~7 GB of pinned host outputs per rank, ~56 GB for the 8 ranks of a node.
+PCIE_FRAMES_MULTI = 480
 
 
 def default_frames_per_step(width: int, height: int) -> int:
@@ -124,29 +127,63 @@ def sum_over_ranks(vals: List[int], world: int) -> List[int]:
     return [int(v) for v in t.tolist()]
 
 
-def shard_report(timed: List[int], world: int, device: Optional[dict] = None) -> dict:
+def shard_report(timed: List[int], world: int, device: Optional[dict] = None, per_rank: Optional[dict] = None) -> dict:
     """Each rank's timed frame ids gathered on every rank (gloo): the seed
     shards must be disjoint, and their union is what ``value`` counts.
     ``device`` (this rank's GPU: ordinal, the process's device count, PCI
     address) is gathered beside them, so a line proves N ranks on N distinct
-    devices -- or says that ranks shared one (a rehearsal on a smaller box)."""
-    lists = [(list(timed), device)]
+    devices -- or says that ranks shared one (a rehearsal on a smaller box).
+    ``per_rank`` (this rank's own timing: elapsed seconds of the timed steps,
+    per-stage ms per step, frames/s) is gathered likewise, so an N > 1 line
+    shows which rank set ``elapsed_max`` and by how much (``imbalance`` =
+    slowest / fastest rank's elapsed time)."""
+    lists = [(list(timed), device, per_rank)]
     if world > 1:
         import torch.distributed as dist
         lists = [None] * world
-        dist.all_gather_object(lists, (list(timed), device))
-    sets = [set(x) for x, _ in lists]
+        dist.all_gather_object(lists, (list(timed), device, per_rank))
+    sets = [set(x) for x, _, _ in lists]
     union = set().union(*sets)
-    rep = {"ranks": world, "timed_frames_per_rank": [len(x) for x, _ in lists],
-           "union": len(union), "disjoint": len(union) == sum(len(x) for x, _ in lists),
-           "epochs_mod_world": [sorted({(f // 10) % world for f in x}) for x, _ in lists]}
-    devs = [d for _, d in lists]
+    rep = {"ranks": world, "timed_frames_per_rank": [len(x) for x, _, _ in lists],
+           "union": len(union), "disjoint": len(union) == sum(len(x) for x, _, _ in lists),
+           "epochs_mod_world": [sorted({(f // 10) % world for f in x}) for x, _, _ in lists]}
+    devs = [d for _, d, _ in lists]
     if all(d is not None for d in devs):
         ids = [d.get("pci") or d["device"] for d in devs]
         rep["devices"] = devs
         rep["distinct_devices"] = len(set(ids))
         rep["shared_devices"] = len(set(ids)) < world
+    prs = [p for _, _, p in lists]
+    if all(p is not None for p in prs):
+        rep["per_rank"] = prs
+        el = [p["elapsed_s"] for p in prs if p.get("elapsed_s")]
+        if el:
+            rep["slowest_rank"] = max(range(len(prs)), key=lambda k: prs[k].get("elapsed_s") or 0.0)
+            rep["imbalance"] = round(max(el) / min(el), 4)
     return rep
+
+
+def gather_delivery(mine: Optional[dict], world: int) -> Optional[dict]:
+    """Host delivery at N > 1: every rank timed its own leg, all started at one
+    barrier.  Per-rank frames/s and GB/s, and the aggregate the N ranks
+    delivered together into host memory: all ranks' frames over the slowest
+    rank's time (what a user of the node's N GPUs gets)."""
+    legs = [mine]
+    if world > 1:
+        import torch.distributed as dist
+        legs = [None] * world
+        dist.all_gather_object(legs, mine)
+    if any(x is None for x in legs):
+        return None
+    t = max(x["seconds"] for x in legs)
+    frames = sum(x["frames"] for x in legs)
+    return {"value": round(frames / t, 2), "unit": "frames/s",
+            "wire_gbs": round(sum(x["wire_bytes"] for x in legs) / t / 1e9, 2),
+            "delivered_gbs": round(sum(x["delivered_bytes"] for x in legs) / t / 1e9, 2),
+            "per_rank": [{"rank": k, "frames_per_s": round(x["frames"] / x["seconds"], 2),
+                          "wire_gbs": round(x["wire_bytes"] / x["seconds"] / 1e9, 2), "frames": x["frames"],
+                          "seconds": round(x["seconds"], 4)} for k, x in enumerate(legs)],
+            "ranks": world}
 
 
 # ---------------------------------------------------------------------------
@@ -232,6 +269,18 @@ def launch_ranks(n: int, child_argv: List[str], env: Optional[Dict[str, str]] = 
                 p.wait()
         for fh in files:
             fh.close()
+
+
+def profiler_preload(env: Dict[str, str]) -> Optional[str]:
+    """Why this process is running under rocprofv3 (its preloaded library
+    initialises the GPU before main), or None."""
+    pre = env.get("LD_PRELOAD", "")
+    if "rocprof" in pre or "roctracer" in pre:
+        return "LD_PRELOAD names the profiler"
+    for k in env:
+        if k.startswith("ROCPROF_") or k.startswith("ROCPROFILER_"):
+            return f"{k} is set"
+    return None
 
 
 def median_time(fn: Callable[[], None], runs: int = 5, warmup: int = 1, what: str = "") -> float:
@@ -405,7 +454,15 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # a plain `python bench.py --gpus N`: start the N ranks here, before
-        # torch is imported (nothing in this process touches the GPU)
+        # torch is imported (nothing in this process touches the GPU) -- unless
+        # a profiler's preloaded library already initialised the GPU in this
+        # process: children started from it would inherit that state and the
+        # preload
+        why = profiler_preload(os.environ)
+        if why:
+            log(f"bench: --gpus {args.gpus} under a profiler ({why}): this process has already initialised the "
+                "GPU, so it cannot start its ranks; profile one rank per command, or put torchrun in front")
+            sys.exit(2)
         sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
 
     rank = int(os.environ.get("RANK", "0"))
@@ -589,11 +646,16 @@ def main():
                     and pj.get("B_frame") == b_geom + b_tex + b_out):
                 traffic = {k: v for k, v in pj.get("bytes_per_launch", {}).items()}
                 work = pj.get("k_raster_work_per_frame")
-                if pj.get("k_raster_valu_busy") is not None:
-                    valu = {"busy": round(pj["k_raster_valu_busy"], 3),
+                if pj.get("k_raster_valu_pipe_occupancy") is not None:
+                    valu = {"pipe_occupancy": round(pj["k_raster_valu_pipe_occupancy"], 3),
+                            "pipe_occupancy_ceiling": pj.get("valu_pipe_ceiling"),
+                            "wave_cycles": pj.get("k_raster_wave_cycles"),
                             "lane_util": round(pj.get("k_raster_valu_lane_util") or 0.0, 3),
-                            "note": "k_raster's limiter: VALU issue (rocprofv3 SQ_ACTIVE_INST_VALU, "
-                                    "profiles/pmc_traffic.json)"}
+                            "note": "calibrated on gfx950 (tools/calib_valu.hip, profiles/r06/calib): VALU pipe "
+                                    "occupancy = SQ_INSTS_VALU x 2 cycles / (1,024 SIMDs x cycles) against the "
+                                    "ceiling 8 waves per SIMD of independent FMAs reach; k_raster's limiter is "
+                                    "latency: the share of its wave-cycles parked on s_waitcnt / s_barrier "
+                                    "(SQ_WAIT_ANY), profiles/pmc_traffic.json"}
         except Exception:
             traffic = valu = work = None
     rf = roofline(b_geom, b_tex, b_out, frames_per_launch, tm["ms_raster"] / launches, tm["ms_setup"] / launches,
@@ -656,7 +718,10 @@ def main():
             v_, p_, ref = ver.render(sample_frames, 2)
             bad = ver.compare(sample_frames, v_, p_, ref, gpu_sample)
     n_checked, n_bad = sum_over_ranks([len(sample_frames), len(bad)], world)
-    shards = shard_report(timed_frames(fids, W, K, F), world, device_info)
+    stage_ms = {k: round(tm[k] / K, 4) for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")}
+    per_rank = {"rank": rank, "elapsed_s": round(elapsed, 6), "frames_per_s": round(K * F / elapsed, 2),
+                "stage_ms_per_step": stage_ms}
+    shards = shard_report(timed_frames(fids, W, K, F), world, device_info, per_rank)
     if n_bad:
         for b in bad[:20]:
             log(f"[rank {rank}] VERIFY FAILED: {b}")
@@ -700,35 +765,71 @@ def main():
         except Exception as e:  # the extra figure must never break the bench line
             log(f"with-stats measurement failed: {e}")
 
-    # ---- PCIe-inclusive rate (rank 0, N=1 only; never `value`) ---------------
+    # ---- host delivery, PCIe included (never `value`) --------------------------
+    # The reference's boundary hands its caller host arrays (get_rgba,
+    # generate_construction_data.py:1669; the int32 mask :1909-1910).  At N = 1
+    # rank 0 times its batches of F frames with host outputs; at N > 1 every rank
+    # does so at once (batches of at most PCIE_FRAMES_MULTI frames, started at one
+    # barrier), since what 8 GPUs deliver into one host's memory is the figure a
+    # user of the node gets.  Instance ids cross PCIe narrowed (csg_host_id_bytes)
+    # and are widened to int32 on host threads inside the timed region.
     pcie = None
-    if rank == 0 and world == 1 and args.pcie_steps > 0:
+    if args.pcie_steps > 0:
+        import ctypes as C
+        from constructionsceneposeestimation_amd import _lib
+        Fp = F if world == 1 else min(F, PCIE_FRAMES_MULTI)
+        leg, idb = None, 4
+        kpb = Kp * 12 if want_kp else 0
         try:
-            import ctypes as C
-            from constructionsceneposeestimation_amd import _lib
-            h_rgb = torch.empty((F, H, Wd, 3), dtype=torch.uint8, pin_memory=True)
-            h_inst = torch.empty((F, H, Wd), dtype=torch.int32, pin_memory=True)
-            h_uv = torch.empty((F, max(Kp, 1), 2), dtype=torch.float32, pin_memory=True)
-            h_vis = torch.empty((F, max(Kp, 1)), dtype=torch.int32, pin_memory=True)
+            h_rgb = torch.empty((Fp, H, Wd, 3), dtype=torch.uint8, pin_memory=True)
+            h_inst = torch.empty((Fp, H, Wd), dtype=torch.int32, pin_memory=True)
+            h_uv = torch.empty((Fp, max(Kp, 1), 2), dtype=torch.float32, pin_memory=True)
+            h_vis = torch.empty((Fp, max(Kp, 1)), dtype=torch.int32, pin_memory=True)
             o = _lib.Outputs(h_rgb.data_ptr(), h_inst.data_ptr(), None, h_uv.data_ptr() if want_kp else None,
                              h_vis.data_ptr() if want_kp else None, None, r.n_labels, 0, None, None)
             # the first step's records as the device holds them: with their work
             # hints (csg_size_work wrote those into frames_dev, not `frames`)
-            hframes = frames_dev[:F * fsz].cpu().numpy().view(FRAME_DTYPE)
-            r._check(r.lib.csg_render_batch_async(r.ctx, hframes.ctypes.data, F, 0, C.byref(o), None), "pcie")
+            hframes = frames_dev[:Fp * fsz].cpu().numpy().view(FRAME_DTYPE)
+
+            def leg():
+                r._check(r.lib.csg_render_batch_async(r.ctx, hframes.ctypes.data, Fp, 0, C.byref(o), None), "pcie")
+            leg()
             r.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(args.pcie_steps):
-                r._check(r.lib.csg_render_batch_async(r.ctx, hframes.ctypes.data, F, 0, C.byref(o), None), "pcie")
-            r.synchronize()
-            dt = time.perf_counter() - t1
-            pcie = {"value": round(args.pcie_steps * F / dt, 2), "unit": "frames/s",
-                    "note": f"outputs (RGB8 + int32 ids + keypoints, {H * Wd * 7 / 1e6:.1f} MB/frame) copied to "
-                            f"pinned host memory inside the timed region (each launch chain's slice on a copy "
-                            f"stream while the next chains render); {args.pcie_steps} batches of {F}",
-                    "gbs": round(args.pcie_steps * F * H * Wd * 7 / dt / 1e9, 2)}
+            idb = r.host_id_bytes()
         except Exception as e:  # the extra figure must never break the bench line
-            log(f"pcie-inclusive measurement failed: {e}")
+            leg = None
+            log(f"[rank {rank}] host-delivery leg setup failed: {e}")
+        if world > 1:
+            dist.barrier()   # every rank starts its leg together (a failed setup still joins)
+        mine = None
+        if leg is not None:
+            try:
+                t1 = time.perf_counter()
+                for _ in range(args.pcie_steps):
+                    leg()
+                r.synchronize()
+                dt = time.perf_counter() - t1
+                nf = args.pcie_steps * Fp
+                mine = {"frames": nf, "seconds": dt, "wire_bytes": nf * (npx * (3 + idb) + kpb),
+                        "delivered_bytes": nf * (npx * 7 + kpb)}
+            except Exception as e:
+                log(f"[rank {rank}] host-delivery measurement failed: {e}")
+        if world > 1:
+            pcie = gather_delivery(mine, world)
+        elif mine is not None:
+            pcie = {"value": round(mine["frames"] / mine["seconds"], 2), "unit": "frames/s",
+                    "wire_gbs": round(mine["wire_bytes"] / mine["seconds"] / 1e9, 2),
+                    "delivered_gbs": round(mine["delivered_bytes"] / mine["seconds"] / 1e9, 2)}
+        if pcie is not None:
+            pcie["gbs"] = pcie["wire_gbs"]
+            pcie["ids_wire_bytes"] = idb
+            pcie["note"] = (f"RGB8 + int32 instance ids + keypoints delivered into pinned host memory inside the timed "
+                            f"region, {args.pcie_steps} batches of {Fp} frames per rank"
+                            + (f", all {world} ranks at once" if world > 1 else "")
+                            + f"; the ids cross PCIe as {idb}-byte values (id + 1) and host threads widen them to "
+                              f"int32 ({npx * (3 + idb) / 1e6:.1f} MB/frame on the wire, "
+                              f"{npx * 7 / 1e6:.1f} MB/frame delivered); each launch chain's slice is copied while "
+                              f"the next chains render")
 
     if rank == 0:
         line = {
@@ -752,7 +853,7 @@ def main():
             "shards": shards,
             "pcie_inclusive": pcie,
             "with_label_stats": with_stats,
-            "stage_ms_per_step": {k: round(tm[k] / K, 4) for k in ("ms_setup", "ms_bin", "ms_raster", "ms_keypoints")},
+            "stage_ms_per_step": stage_ms,
             "work": {"bytes": int(winfo["work_bytes"]), "contexts": NC,
                      "pool_records": int(winfo["pool_records"]), "pool_bins": int(winfo["pool_bins"]),
                      "hinted": bool(winfo["hinted"]), "hint_retries": int(r.work_info()["hint_retries"]),

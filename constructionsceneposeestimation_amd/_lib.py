@@ -25,7 +25,7 @@ EXPORTED = (
     "csg_render_batch", "csg_render_batch_async", "csg_synchronize", "csg_get_batch_stats",
     "csg_project_keypoints", "csg_timing_reset", "csg_timing_read", "csg_set_dr_light", "csg_set_dr_textures",
     "csg_instance_bounds", "csg_copy_files", "csg_host_alloc", "csg_host_free", "csg_size_work",
-    "csg_get_work_info",
+    "csg_get_work_info", "csg_host_id_bytes",
 )
 
 
@@ -140,6 +140,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib.csg_last_error.argtypes = [vp]
     lib.csg_last_error.restype = C.c_char_p
     lib.csg_abi_version.argtypes = []
+    lib.csg_host_id_bytes.argtypes = [vp]
     lib.csg_upload_scene.argtypes = [vp, C.POINTER(Mesh), u32, C.POINTER(Material), u32, C.POINTER(Instance), u32]
     lib.csg_upload_texture.argtypes = [vp, u32, vp, u32, u32]
     lib.csg_set_light.argtypes = [vp, C.POINTER(Light)]

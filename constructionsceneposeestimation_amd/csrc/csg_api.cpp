@@ -11,16 +11,19 @@
 #include <string.h>
 
 #include <algorithm>
+#include <numeric>
 #include <cstddef>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/csg_api.h"
 #include "csg_encode.h"
 #include "csg_kernels.h"
+#include "csg_widen.h"
 
 using namespace csg;
 
@@ -203,6 +206,16 @@ struct csg_ctx {
   hipStream_t copy_stream = nullptr;
   hipEvent_t copy_ev[kCopyEv] = {};
   hipEvent_t copy_done = nullptr;
+  // The host wire of the instance ids (csg_widen.h): a host-output batch's ids
+  // cross PCIe as (id + 1) in ids_bytes (1 with at most 255 labels, 2 with at
+  // most 65,535; 4 = int32 as rendered, no narrowing) and are widened to the
+  // caller's int32 by WidenPool threads while later chains render.
+  // CSG_NARROW_IDS=0 keeps int32 on the wire (A/B, tests).
+  uint32_t ids_bytes = 4;               // set by csg_upload_scene from the label range
+  bool narrow_ids = true;
+  DevBuf<uint8_t> o_ids_n;              // [F][H][W] narrowed ids (device)
+  uint8_t* h_ids_n = nullptr;           // ... their pinned host landing buffer
+  size_t h_ids_n_bytes = 0;
   // the last sizing pass (csg_size_work)
   uint32_t sized_frames = 0, sized_max_rec = 0, sized_max_bin = 0;
   double sized_mean_rec = 0.0, sized_mean_bin = 0.0;
@@ -295,14 +308,16 @@ const char* csg_last_error(const csg_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int csg_create(const csg_config* cfg, csg_ctx** out) {
   if (!cfg || !out) return CSG_ERR_INVALID;
   *out = nullptr;
-  // tile rectangles carry 8-bit tile coordinates (k_setup's rect, k_count / k_bin): at most 256 x 256 tiles
-  if (cfg->width == 0 || cfg->height == 0 || cfg->width > 256u * kTileW || cfg->height > 256u * kTileH ||
+  // tile rectangles carry 8-bit tile coordinates (k_setup's rect, k_count / k_bin): at most 256 tile columns
+  // and 512 tile rows (rows in pairs above 256: 8,192 x 8,192 px at 32 x 16 tiles)
+  if (cfg->width == 0 || cfg->height == 0 || cfg->width > 256u * kTileW || cfg->height > 512u * kTileH ||
       cfg->max_frames == 0 ||
       !(cfg->near_clip >= 0x1p-126f) || !(cfg->far_clip > cfg->near_clip) || !(cfg->far_clip <= 0x1p126f))
     return CSG_ERR_INVALID;   // clip distances in [2^-126, 2^126]: the range of rcp_ieee's proof (k_setup, k_raster)
   csg_ctx* c = new csg_ctx();
   c->cfg = *cfg;
   if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
+  if (const char* v = getenv("CSG_NARROW_IDS")) c->narrow_ids = atoi(v) != 0;
   c->chain_frames = cfg->frames_per_launch ? cfg->frames_per_launch : kAutoChainFrames;
   if (const char* v = getenv("CSG_CHAIN")) c->chain_frames = (uint32_t)std::max(1, atoi(v));
   c->chain_frames = std::min(c->chain_frames, cfg->max_frames);
@@ -362,7 +377,9 @@ void csg_destroy(csg_ctx* c) {
   }
   for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
-  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);   // (widening included: see enqueue_batch)
+  if (c->h_ids_n) (void)hipHostFree(c->h_ids_n);
+  c->o_ids_n.release();
   for (auto& e : c->copy_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->copy_done) (void)hipEventDestroy(c->copy_done);
@@ -475,6 +492,11 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   HIP_TRY(c, hipMemcpy(c->tri_uv.p, tri_uv.data(), tri_uv.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->inst.p, idesc.data(), idesc.size() * sizeof(InstDesc), hipMemcpyHostToDevice));
   c->h_inst = idesc;
+  {   // the ids the resolve writes are instance labels and -1: the narrowest host wire for them
+    int32_t lo = -1, hi = -1;
+    for (const InstDesc& d : idesc) { lo = std::min(lo, d.label); hi = std::max(hi, d.label); }
+    c->ids_bytes = lo < -1 ? 4u : hi <= 254 ? 1u : hi <= 65534 ? 2u : 4u;
+  }
   c->iset.release();   // rebuilt for the new instances by the next sync_scene_state
   HIP_TRY(c, hipMemcpy(c->chunks.p, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice));
   c->n_inst = n_inst;
@@ -834,7 +856,39 @@ static SceneDev scene_dev(const csg_ctx* c) {
   s.inv_near = 1.0f / c->cfg.near_clip; s.inv_far = 1.0f / c->cfg.far_clip;
   s.dbg = c->dbg;
   s.uid_shift = c->uid_shift;
+  s.rect_ys = c->tiles_y > 256u ? 1u : 0u;   // tile rectangles of taller frames hold tile-row pairs
   return s;
+}
+
+// Page-locked host memory (hipHostMalloc / hipHostRegister): only then is a
+// D2H hipMemcpyAsync asynchronous; a pageable destination is staged and blocks.
+static bool host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Host functions on the copy stream (csg_widen.h): a chain's narrowed ids are
+// handed to the widening pool once their copy has landed; the batch's last
+// host function waits for all of them, so the copy stream -- and the batch's
+// stream, which waits on it -- completes only after the int32 ids are written.
+struct WidenChain {
+  const void* src;
+  uint32_t bytes;
+  int32_t* dst;
+  size_t n;
+  std::shared_ptr<WidenLatch> latch;
+};
+static void widen_submit_cb(void* p) {
+  std::unique_ptr<WidenChain> w(static_cast<WidenChain*>(p));
+  WidenPool::get().submit(w->src, w->bytes, w->dst, w->n, w->latch);
+}
+static void widen_wait_cb(void* p) {
+  std::unique_ptr<std::shared_ptr<WidenLatch>> l(static_cast<std::shared_ptr<WidenLatch>*>(p));
+  (*l)->wait();
 }
 
 // fk: file kinds the batch's images will be encoded to (csg_render_batch):
@@ -995,15 +1049,48 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   // chains are at most an eighth of the batch (>= kMinCopyChain frames) and each
   // chain's outputs cross PCIe on the copy stream while the next chains render:
   // the batch then costs about its copies plus one chain's render, not the sum.
+  // Chains split for copying only when every host destination is page-locked
+  // (a pageable copy blocks the host until it is done, so later chains would
+  // not render under it: ADVICE r05).  Narrowed ids land in the context's own
+  // page-locked buffer, whatever the caller's int32 array is.
   constexpr uint32_t kCopyChunks = 8, kMinCopyChain = 32;
   uint32_t G = c->chain_frames;
+  const bool narrow = !dev && out->instance && c->narrow_ids && c->ids_bytes < 4;
   if (!dev) {
-    G = std::min(G, std::max(kMinCopyChain, (F + kCopyChunks - 1) / kCopyChunks));
+    bool pinned = true;
+    const void* dsts[] = {out->rgb, narrow ? nullptr : out->instance, out->depth, out->normals, out->points,
+                          out->inst_stats, out->label_covered, out->depth_vis, out->depth_range, out->depth_stats,
+                          want_kp ? out->keypoints_uv : nullptr, want_kp ? out->keypoints_vis : nullptr};
+    for (const void* d : dsts) pinned = pinned && (!d || host_pinned(d));
+    if (pinned) G = std::min(G, std::max(kMinCopyChain, (F + kCopyChunks - 1) / kCopyChunks));
     if (!c->copy_stream) {
       HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
       for (auto& e : c->copy_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
       HIP_TRY(c, hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming));
     }
+  }
+  // k_raster's 4-pixel vector stores test alignment relative to the chain's
+  // first pixel: chains start at pixel c0 * npx, a multiple of 4 when G is a
+  // multiple of 4 / gcd(npx, 4) (F = G frames otherwise)
+  {
+    const uint32_t m = 4u / (uint32_t)std::gcd<size_t>(npx, 4);
+    if (G < F) G = std::min(F, (G + m - 1) / m * m);
+  }
+  std::shared_ptr<WidenLatch> latch;
+  if (narrow) {
+    const size_t nb = (size_t)F * npx * c->ids_bytes;
+    HIP_TRY(c, c->o_ids_n.alloc(nb));
+    if (c->h_ids_n_bytes < nb) {
+      if (c->h_ids_n) {   // the previous batch's widening (on the copy stream) may still read it
+        HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
+        HIP_TRY(c, hipHostFree(c->h_ids_n));
+        c->h_ids_n = nullptr;
+        c->h_ids_n_bytes = 0;
+      }
+      HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_ids_n), nb, hipHostMallocDefault));
+      c->h_ids_n_bytes = nb;
+    }
+    latch = std::make_shared<WidenLatch>();
   }
   HIP_TRY(c, hipMemsetAsync(c->plan_need.p, 0, 2 * sizeof(uint64_t), st));   // k_plan: max over the chains
   for (uint32_t c0 = 0, chain = 0; c0 < F; c0 += G, ++chain) {
@@ -1062,6 +1149,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       }
     }
     c->last_F = Fc;
+    if (narrow) launch_narrow_ids(b.inst, (size_t)c0 * npx, (size_t)(c0 + Fc) * npx, c->ids_bytes, c->o_ids_n.p, st);
     if (!dev) {   // this chain's outputs to the host, on the copy stream, behind its kernels
       hipEvent_t e = c->copy_ev[chain % csg_ctx::kCopyEv];
       hipStream_t cs = c->copy_stream;
@@ -1073,7 +1161,17 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
                               hipMemcpyDeviceToHost, cs);
       };
       if (out->rgb) HIP_TRY(c, copy(out->rgb, b.rgb, npx * 3));
-      if (out->instance) HIP_TRY(c, copy(out->instance, b.inst, npx * 4));
+      if (narrow) {   // (id + 1) bytes to the landing buffer, then widened into the caller's int32 ids
+        const size_t pf = npx * c->ids_bytes;
+        HIP_TRY(c, copy(c->h_ids_n, c->o_ids_n.p, pf));
+        auto* w = new WidenChain{c->h_ids_n + (size_t)c0 * pf, c->ids_bytes, out->instance + (size_t)c0 * npx,
+                                 (size_t)Fc * npx, latch};
+        const hipError_t he = hipLaunchHostFunc(cs, widen_submit_cb, w);
+        if (he != hipSuccess) delete w;
+        HIP_TRY(c, he);
+      } else if (out->instance) {
+        HIP_TRY(c, copy(out->instance, b.inst, npx * 4));
+      }
       if (out->depth) HIP_TRY(c, copy(out->depth, b.depth, npx * 4));
       if (out->normals) HIP_TRY(c, copy(out->normals, b.normals, npx * 6));
       if (out->points) HIP_TRY(c, copy(out->points, b.points, npx * 12));
@@ -1092,6 +1190,12 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
   c->last_points = b.points;
   c->last_dvis = dvis;
   if (!dev) {   // the batch's stream orders everything after it (and csg_synchronize) behind the copies
+    if (narrow) {   // ... and behind the widening of every chain's ids
+      auto* l = new std::shared_ptr<WidenLatch>(latch);
+      const hipError_t he = hipLaunchHostFunc(c->copy_stream, widen_wait_cb, l);
+      if (he != hipSuccess) delete l;
+      HIP_TRY(c, he);
+    }
     HIP_TRY(c, hipEventRecord(c->copy_done, c->copy_stream));
     HIP_TRY(c, hipStreamWaitEvent(st, c->copy_done, 0));
   }
@@ -1571,6 +1675,11 @@ int csg_get_work_info(csg_ctx* c, csg_work_info* out) {
   if (!c || !out) return CSG_ERR_INVALID;
   fill_work_info(c, out);
   return CSG_OK;
+}
+
+int csg_host_id_bytes(const csg_ctx* c) {
+  if (!c) return CSG_ERR_INVALID;
+  return c->narrow_ids ? (int)c->ids_bytes : 4;
 }
 
 int csg_project_keypoints(csg_ctx* c, const float* pts, uint32_t n, const float* view, const float* proj, float* uv_out,

@@ -137,6 +137,7 @@ struct SceneDev {
   // instance the soup index is the mesh's base plus the triangle), and the
   // resolve finds the triangle without loading the instance first.
   uint32_t uid_shift;
+  uint32_t rect_ys;            // tile rectangles hold tile-row pairs (1: more than 256 tile rows) or rows (0)
 };
 
 // Bits of overflow[0] (sticky until csg_synchronize / csg_render_batch reads them)
@@ -224,5 +225,7 @@ void launch_inst_bounds(const SceneDev& s, const Chunk* chunks, uint32_t n_chunk
                         uint32_t* out, hipStream_t st);
 void launch_project(const float* pts, uint32_t n, const float* pv12, float W, float H, float near_clip,
                     float* uv, int32_t* vis, hipStream_t st);
+// ids [lo, hi) of the int32 instance image as (id + 1) in `bytes` (1 or 2) bytes (the host wire)
+void launch_narrow_ids(const int32_t* src, size_t lo, size_t hi, uint32_t bytes, void* dst, hipStream_t st);
 
 }  // namespace csg

@@ -452,14 +452,26 @@ __device__ __forceinline__ bool make_rec(const SceneDev& s, const float* su, con
   return true;
 }
 
-__device__ __forceinline__ uint32_t rec_tile_rect(const SubRec& r) {
+// Tile rectangle of a record: tx0 | ty0 << 8 | tx1 << 16 | ty1 << 24, 8-bit
+// tile coordinates.  Frames of more than 256 tile rows (taller than 4,096 px
+// at 32 x 16; at most 512 rows) store tile-row PAIRS (ys = 1, SceneDev::
+// rect_ys): the record is binned to both tiles of every pair its box touches,
+// a superset the raster's per-tile row clipping makes harmless (a record
+// binned to a tile it misses stages no rows), so outputs do not change.
+__device__ __forceinline__ uint32_t rec_tile_rect(const SubRec& r, uint32_t ys) {
   const uint32_t px0 = r.g1.z & 0xFFFFu, py0 = r.g1.z >> 16, px1 = r.g1.w & 0xFFFFu, py1 = r.g1.w >> 16;
-  return (px0 / kTileW) | ((py0 / kTileH) << 8) | ((px1 / kTileW) << 16) | ((py1 / kTileH) << 24);
+  return (px0 / kTileW) | (((py0 / kTileH) >> ys) << 8) | ((px1 / kTileW) << 16) | (((py1 / kTileH) >> ys) << 24);
 }
 
-__device__ __forceinline__ uint32_t rect_area(uint32_t rc) {
-  const uint32_t tx0 = rc & 255u, ty0 = (rc >> 8) & 255u, tx1 = (rc >> 16) & 255u, ty1 = rc >> 24;
-  return (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+// first and last tile row of a rectangle (rows past the frame's last dropped)
+__device__ __forceinline__ uint32_t rect_ty0(uint32_t rc, uint32_t ys) { return ((rc >> 8) & 255u) << ys; }
+__device__ __forceinline__ uint32_t rect_ty1(uint32_t rc, uint32_t ys, uint32_t tiles_y) {
+  return min((((rc >> 24) + 1u) << ys) - 1u, tiles_y - 1u);
+}
+
+__device__ __forceinline__ uint32_t rect_area(uint32_t rc, uint32_t ys, uint32_t tiles_y) {
+  const uint32_t tx0 = rc & 255u, tx1 = (rc >> 16) & 255u;
+  return (tx1 - tx0 + 1) * (rect_ty1(rc, ys, tiles_y) - rect_ty0(rc, ys) + 1);
 }
 
 // q / w for q < 2^24, 1 <= w <= 256: float reciprocal estimate (off by at
@@ -471,8 +483,8 @@ __device__ __forceinline__ uint32_t small_div(uint32_t q, uint32_t w) {
   return d;
 }
 
-__device__ __forceinline__ uint32_t rect_tile(uint32_t rc, uint32_t q, uint32_t tiles_x) {
-  const uint32_t tx0 = rc & 255u, ty0 = (rc >> 8) & 255u, tx1 = (rc >> 16) & 255u;
+__device__ __forceinline__ uint32_t rect_tile(uint32_t rc, uint32_t q, uint32_t tiles_x, uint32_t ys) {
+  const uint32_t tx0 = rc & 255u, ty0 = rect_ty0(rc, ys), tx1 = (rc >> 16) & 255u;
   const uint32_t w = tx1 - tx0 + 1;
   const uint32_t r = small_div(q, w);
   return __umul24(ty0 + r, tiles_x) + tx0 + (q - __umul24(r, w));
@@ -689,8 +701,8 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
-  if (nrec > 0 && wbase + mine < rcap) b.rect[rbase + wbase + mine] = rec_tile_rect(r0);
-  if (nrec > 1 && wbase + mine + 1 < rcap) b.rect[rbase + wbase + mine + 1] = rec_tile_rect(r1);
+  if (nrec > 0 && wbase + mine < rcap) b.rect[rbase + wbase + mine] = rec_tile_rect(r0, s.rect_ys);
+  if (nrec > 1 && wbase + mine + 1 < rcap) b.rect[rbase + wbase + mine + 1] = rec_tile_rect(r1, s.rect_ys);
 }
 
 // ---------------------------------------------------------------------------
@@ -735,7 +747,7 @@ __device__ __forceinline__ int find_bin_item(const uint32_t* pre, uint32_t j) {
 constexpr uint32_t kCountDirect = 4;
 template <uint32_t kDirect, typename Single>
 __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32_t base, uint32_t n, uint32_t* lrc,
-                                                    uint32_t* pre, uint32_t* wsum, uint32_t tiles_x, Single single) {
+                                                    uint32_t* pre, uint32_t* wsum, const SceneDev& s, Single single) {
   const int tid = threadIdx.x;
   const uint32_t r0 = base + (uint32_t)tid * kBinRpt;
   uint32_t rc[kBinRpt], area[kBinRpt], sum = 0;
@@ -751,11 +763,11 @@ __device__ __forceinline__ uint32_t bin_round_setup(const uint32_t* rect, uint32
   rc[0] = v.x; rc[1] = v.y; rc[2] = v.z; rc[3] = v.w;
 #pragma unroll
   for (int q = 0; q < kBinRpt; ++q) {
-    area[q] = (r0 + (uint32_t)q < n) ? rect_area(rc[q]) : 0u;
+    area[q] = (r0 + (uint32_t)q < n) ? rect_area(rc[q], s.rect_ys, s.tiles_y) : 0u;
     lrc[tid * kBinRpt + q] = rc[q];
     if (kDirect && area[q] && area[q] <= kDirect) {
 #pragma clang loop unroll(disable)
-      for (uint32_t a = 0; a < area[q]; ++a) single(q, rect_tile(rc[q], a, tiles_x));
+      for (uint32_t a = 0; a < area[q]; ++a) single(q, rect_tile(rc[q], a, s.tiles_x, s.rect_ys));
       area[q] = 0u;
     }
   }
@@ -794,14 +806,14 @@ __global__ __launch_bounds__(256) void k_count(SceneDev s, BatchDev b) {
     for (uint32_t t = tid; t < nb; t += kBlock) hist[t] = 0;
     __syncthreads();
     for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-      const uint32_t total = bin_round_setup<kCountDirect>(rect, base, n, lrc, pre, wsum, s.tiles_x,
+      const uint32_t total = bin_round_setup<kCountDirect>(rect, base, n, lrc, pre, wsum, s,
                                                    [&](int, uint32_t t) {
                                                      if (!kBanded || t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
                                                    });
       __syncthreads();
       for (uint32_t j = tid; j < total; j += kBlock) {
         const int k = find_bin_item(pre, j);
-        const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
+        const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x, s.rect_ys);
         if (!kBanded || t - t0 < nb) atomicAdd(&hist[t - t0], 1u);
       }
       __syncthreads();
@@ -941,11 +953,11 @@ __global__ __launch_bounds__(256) void k_bin(SceneDev s, BatchDev b) {
       hist[t] = toff[t0 + t] + tcnt[t0 + t] - bo[t0 + t] - 1u;   // last slot of the mirrored range; decremented
     __syncthreads();
     for (uint32_t base = blockIdx.x * kBinRound; base < n; base += gridDim.x * kBinRound) {
-      const uint32_t total = bin_round_setup<0>(rect, base, n, lrc, pre, wsum, s.tiles_x, [](int, uint32_t) {});
+      const uint32_t total = bin_round_setup<0>(rect, base, n, lrc, pre, wsum, s, [](int, uint32_t) {});
       __syncthreads();
       for (uint32_t j = tid; j < total; j += kBlock) {
         const int k = find_bin_item(pre, j);
-        const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x);
+        const uint32_t t = rect_tile(lrc[k], j - pre[k], s.tiles_x, s.rect_ys);
         if (!kBanded || t - t0 < nb) {
           const uint32_t slot = atomicSub(&hist[t - t0], 1u);
           if (slot < sb.bin_cap) bins[slot] = base + (uint32_t)k;
@@ -1034,6 +1046,31 @@ __device__ __forceinline__ void row_span(const uint4& g0, const uint4& g1, int o
   }
 }
 
+#ifndef CSG_WR_DEBUG
+#define CSG_WR_DEBUG 0   // debug builds only: check every span end and fragment with the exact edge test
+#endif
+// The spec's exact coverage of tile pixel (lx, ly) by a staged record (int64, as row_span<false>).
+__device__ __forceinline__ bool exact_cover(const uint4& g0, const uint4& g1, int ox, int oy, int lx, int ly) {
+  const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
+  const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
+  const int64_t cx = (int64_t)(ox + lx) * 256 + 128, cy = (int64_t)(oy + ly) * 256 + 128;
+  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
+  bool in = true;
+  for (int e = 0; e < 3; ++e) {
+    const int64_t ax = RX[ea[e]], ay = RY[ea[e]], dx = (int64_t)RX[eb[e]] - ax, dy = (int64_t)RY[eb[e]] - ay;
+    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
+    in &= dx * (cy - ay) - dy * (cx - ax) + bias >= 0;
+  }
+  return in;
+}
+__device__ __forceinline__ void wr_debug_report(uint32_t* ov, uint32_t what, uint32_t a, uint32_t b2, uint32_t c2,
+                                                uint32_t d, uint32_t e) {
+  atomicAdd(&ov[what], 1u);
+  if (atomicCAS(&ov[7], 0u, what) == 0u) {
+    ov[8] = a; ov[9] = b2; ov[10] = c2; ov[11] = d; ov[12] = e;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
@@ -1072,7 +1109,7 @@ static_assert(kStage <= kRasterBlock && CSG_COV_STAGE <= kRasterBlock, "one stag
 constexpr int kRB = kRasterBlock;
 // level-2 items of one level-1 round: up to kRB spans of up to kTileW pixels,
 // as 32-item words of the start bitmap
-constexpr int kL2Words = kRB * kTileW / 32;
+[[maybe_unused]] constexpr int kL2Words = kRB * kTileW / 32;
 constexpr int kColWords = (kTileW + 31) / 32;   // 32-bit column masks per tile row (label statistics)
 template <bool kCov>
 constexpr int kStageOf = kCov ? CSG_COV_STAGE : kStage;
@@ -1235,11 +1272,20 @@ __device__ __forceinline__ void fragment(const RasterCtx& c, const RecImage<NS>&
 
 // Stage bin entry `idx` into `slot`; returns its row count inside the tile.
 template <int NS>
+__device__ __forceinline__ uint32_t stage_record_r(const Rec* recs, uint32_t r, uint32_t rec_cap, RecImage<NS>& img,
+                                                   int slot, int ox, int oy, uint32_t& row0);
+template <int NS>
 __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t* bins, uint32_t idx, uint32_t end,
                                                  uint32_t rec_cap, RecImage<NS>& img, int slot, int ox, int oy,
                                                  uint32_t& row0) {
-  row0 = 0;
   const uint32_t r = (idx < end && slot < NS) ? bins[idx] : 0xFFFFFFFFu;
+  return stage_record_r<NS>(recs, r, rec_cap, img, slot, ox, oy, row0);
+}
+// ... with the record id `r` already loaded (kNoRecord: none)
+template <int NS>
+__device__ __forceinline__ uint32_t stage_record_r(const Rec* recs, uint32_t r, uint32_t rec_cap, RecImage<NS>& img,
+                                                   int slot, int ox, int oy, uint32_t& row0) {
+  row0 = 0;
   if (r >= rec_cap) return 0;
   const uint4* src = reinterpret_cast<const uint4*>(recs + r);
   uint4 q[kRecGroups];
@@ -1298,6 +1344,198 @@ __device__ __forceinline__ uint32_t stage_record(const Rec* recs, const uint32_t
   return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
 
+// Wave-private rows (CSG_WAVE_ROWS, round 6): after the one barrier that ends
+// a batch's staging, wave w of the workgroup owns the tile rows ly = w (mod
+// kNW) -- interleaved, so a batch's rows split evenly -- and runs level 1
+// and level 2 of those rows alone: its (record, row) items, its spans and its
+// fragments, with wave-level DPP scans and its own bookkeeping in LDS.  No
+// other wave reads or writes its z-buffer rows or its bookkeeping, so there is
+// no s_barrier until the next batch is staged (the block-wide version crosses
+// two per batch and three per level-1 round).  Lanes of one wave see each
+// other's LDS writes in program order (the LDS executes a wave's instructions
+// in order); wave_lds_order() only keeps the compiler from moving accesses
+// across those hand-offs.
+#ifndef CSG_WAVE_ROWS
+#define CSG_WAVE_ROWS 0
+#endif
+#ifndef CSG_PREFETCH_BIN
+#define CSG_PREFETCH_BIN 0     // A/B: the block version's record ids one batch ahead
+#endif
+constexpr int kNW = kRB / 64;                      // waves per raster workgroup
+constexpr int kRowsW = kTileH / kNW;               // tile rows each wave owns
+static_assert((kNW & (kNW - 1)) == 0 && kTileH % kNW == 0, "rows split evenly over the waves");
+#ifndef CSG_WAVE_ORDER_WAIT
+#define CSG_WAVE_ORDER_WAIT 0
+#endif
+__device__ __forceinline__ void wave_lds_order() {
+  if (CSG_WAVE_ORDER_WAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// exclusive wave64 scan; `total` = the wave's sum (lane 63's inclusive value)
+#ifndef CSG_WR_HALVES
+#define CSG_WR_HALVES 0    // A/B: wave w owns rows [w * kRowsW, (w + 1) * kRowsW) instead of ly = w (mod kNW)
+#endif
+#ifndef CSG_WR_SHFL
+#define CSG_WR_SHFL 0
+#endif
+#ifndef CSG_WR_CHECK
+#define CSG_WR_CHECK 0
+#endif
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total, uint32_t* flag = nullptr) {
+  const uint32_t inc = wave_incl_scan(v);
+  total = CSG_WR_SHFL ? (uint32_t)__shfl((int)inc, 63, 64) : (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+  if (CSG_WR_CHECK && flag) {
+    const uint32_t t2 = (uint32_t)__shfl((int)inc, 63, 64);
+    if (t2 != total && (threadIdx.x & 63) == 0) atomicOr(flag, 64u);
+  }
+  return inc - v;
+}
+// one wave's level-1 / level-2 bookkeeping (NS <= 64 staged records: one per lane)
+template <int NS>
+struct WaveLds {
+  static constexpr int kW1 = (NS * kRowsW + 31) / 32;   // level-1 item words (<= NS * kRowsW items)
+  static constexpr int kW2 = 64 * kTileW / 32;          // level-2 item words (<= 64 spans of <= kTileW px)
+  uint32_t crec[NS];          // compact record: slot | first item << 8 | first row << 18 | small << 23
+  uint32_t span[64];          // rec | ly << 8 | (ex2 - xl + kTileW) << 16
+  uint32_t starts1[kW1];      // bit i: a record's rows start at level-1 item i
+  uint32_t starts[kW2];       // bit i: a span starts at level-2 item i
+  uint8_t before1[kW1 + 1];   // records starting before item 32*d (<= NS <= 64)
+  uint8_t before[kW2 + 1];    // spans starting before item 32*d (<= 64)
+};
+
+#if CSG_WAVE_ROWS
+template <int NS>
+struct RasterLds {
+  static_assert(NS <= 64, "wave-private rows: one staged record per lane");
+  RecImage<NS> img;                     // staged bin records
+  uint16_t rinfo[NS];                   // first tile row | 0x80 if small | row count << 8
+  WaveLds<NS> w[kNW];
+};
+
+template <bool kCov, int NS>
+__device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev& s, const BatchDev& b, RasterLds<NS>& L,
+                                             uint32_t beg, uint32_t end, const uint32_t* bins, const Rec* recs,
+                                             uint32_t rec_cap, uint32_t) {
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  WaveLds<NS>& V = L.w[wv];
+  for (uint32_t base = beg; base < end; base += NS) {
+    if (base != beg) __syncthreads();   // every wave is done with the previous batch's image
+    uint32_t row0;
+    const uint32_t rows = stage_record(recs, bins, base + tid, end, rec_cap, L.img, tid, c.ox, c.oy, row0);
+    if (tid < NS) L.rinfo[tid] = (uint16_t)(row0 | (rows << 8));
+    if constexpr (kCov) {   // label of the staged record (read back from this thread's own slot)
+      if (tid < NS) {
+        int32_t lab = -1;
+        if (rows) {
+          lab = s.inst[L.img.q[2][tid].x >> s.uid_shift].label;
+          if (lab >= 0 && (uint32_t)lab >= b.n_labels) lab = -1;
+        }
+        c.rlabel[tid] = lab;
+      }
+    }
+    if ((DBG(b.dbg) & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
+      atomicAdd(&b.overflow[1], 1u);
+      atomicAdd(&b.overflow[2], rows);
+    }
+    __syncthreads();
+    // this wave's rows of record `lane`: ly = wv (mod kNW) inside [a, a + n)
+    uint32_t cnt = 0, fr = 0, sm = 0;
+    if (lane < (uint32_t)NS) {
+      const uint32_t ri = L.rinfo[lane], a = ri & 31u, n = ri >> 8;
+      sm = (ri >> 7) & 1u;
+#if CSG_WR_HALVES
+      fr = max(a, wv * (uint32_t)kRowsW);
+      const uint32_t last = min(a + n, (wv + 1u) * (uint32_t)kRowsW);
+      cnt = n && fr < last ? last - fr : 0u;
+#else
+      fr = a + ((wv - a) & (uint32_t)(kNW - 1));
+      cnt = fr < a + n ? (a + n - 1u - fr) / (uint32_t)kNW + 1u : 0u;
+#endif
+    }
+    if (lane < (uint32_t)WaveLds<NS>::kW1) V.starts1[lane] = 0u;
+    if (lane == 0) V.before1[0] = 0;
+    uint32_t tot1p;
+    const uint32_t ex1p = wave_excl_scan(cnt | (cnt ? 0x10000u : 0u), tot1p, b.overflow);
+    const uint32_t tot1 = tot1p & 0xFFFFu;
+    wave_lds_order();
+    if (cnt) {
+      const uint32_t ex1 = ex1p & 0xFFFFu, ci = ex1p >> 16, e_end = ex1 + cnt;
+      V.crec[ci] = lane | (ex1 << 8) | (fr << 18) | (sm << 23);
+      atomicOr(&V.starts1[ex1 >> 5], 1u << (ex1 & 31u));
+      if ((e_end & ~31u) > ex1) V.before1[e_end >> 5] = (uint8_t)(ci + 1u);   // cnt <= kRowsW <= 32
+    }
+    wave_lds_order();
+    for (uint32_t c1 = 0; c1 < ((DBG(b.dbg) & 256u) ? 0u : tot1); c1 += 64u) {
+      const uint32_t j1 = c1 + lane;
+      uint32_t w2 = 0, sp = 0;
+      int xl = 0;
+      if (j1 < tot1) {
+        const uint32_t w1 = V.starts1[j1 >> 5], nb1 = V.before1[j1 >> 5];
+        const uint32_t cr = V.crec[nb1 + (uint32_t)__popc(w1 & (0xFFFFFFFFu >> (31u - (j1 & 31u)))) - 1u];
+        const int k = (int)(cr & 255u);
+        const uint32_t first = (cr >> 8) & 1023u;
+        const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
+        const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTileW - 1);
+        const int ly = (int)((cr >> 18) & 31u) + (CSG_WR_HALVES ? 1 : kNW) * (int)(j1 - first);
+        int xr;
+        if (DBG(b.dbg) & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
+        else if (cr & (1u << 23)) row_span<true>(g0, g1, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
+        else {
+          if (DBG(b.dbg) & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
+          row_span<false>(g0, g1, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
+        }
+        if (xl <= xr) {
+          w2 = (uint32_t)(xr - xl + 1);
+          sp = (uint32_t)k | ((uint32_t)ly << 8);
+          if (CSG_WR_DEBUG && (!exact_cover(g0, g1, c.ox, c.oy, xl, ly) || !exact_cover(g0, g1, c.ox, c.oy, xr, ly)))
+            wr_debug_report(b.overflow, 1u, (uint32_t)c.ox | ((uint32_t)c.oy << 16), (uint32_t)k | (wv << 8) | (cr & 0x800000u),
+                            (uint32_t)ly | ((uint32_t)xl << 8) | ((uint32_t)xr << 16), j1 | (first << 16), g1.z);
+        }
+      }
+      if ((DBG(b.dbg) & 512u) && w2) {      // non-empty spans, level-2 items
+        atomicAdd(&b.overflow[3], 1u);
+        atomicAdd(&b.overflow[4], w2);
+      }
+      // the chunk's non-empty spans: compact index and item offset from one
+      // packed wave scan; item -> span by a rank query (as the block version)
+#pragma unroll
+      for (int w = 0; w < WaveLds<NS>::kW2; w += 64) V.starts[w + (int)lane] = 0u;
+      if (lane == 0) V.before[0] = 0;
+      uint32_t totp;
+      const uint32_t exp = wave_excl_scan(w2 | (w2 ? 0x10000u : 0u), totp, b.overflow);
+      const uint32_t ex2 = exp & 0xFFFFu, tot2 = totp & 0xFFFFu;
+      wave_lds_order();
+      if (w2) {
+        const uint32_t ci = exp >> 16, e_end = ex2 + w2;
+        V.span[ci] = sp | ((ex2 - (uint32_t)xl + (uint32_t)kTileW) << 16);
+        atomicOr(&V.starts[ex2 >> 5], 1u << (ex2 & 31u));
+        if constexpr (kTileW <= 32) {
+          if ((e_end & ~31u) > ex2) V.before[e_end >> 5] = (uint8_t)(ci + 1u);
+        } else {
+          for (uint32_t d = (ex2 >> 5) + 1u; d <= (e_end >> 5); ++d) V.before[d] = (uint8_t)(ci + 1u);
+        }
+      }
+      wave_lds_order();
+      for (uint32_t j = lane; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += 64u) {
+        const uint32_t w = V.starts[j >> 5], nb = V.before[j >> 5];
+        const uint32_t rank = nb + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31u - (j & 31u))));
+        const uint32_t spj = V.span[rank - 1u];
+        if (CSG_WR_DEBUG) {
+          const int kk = (int)(spj & 255u), lx = (int)(j + (uint32_t)kTileW - (spj >> 16)), ly = (int)((spj >> 8) & 255u);
+          if (lx < 0 || lx >= kTileW || !exact_cover(L.img.q[0][kk], L.img.q[1][kk], c.ox, c.oy, lx, ly))
+            wr_debug_report(b.overflow, 2u, (uint32_t)c.ox | ((uint32_t)c.oy << 16), (uint32_t)kk | (wv << 8),
+                            (uint32_t)ly | ((uint32_t)(lx & 255) << 8), j | (rank << 16), tot2);
+        }
+        fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + (uint32_t)kTileW - (spj >> 16)), (int)((spj >> 8) & 255u));
+      }
+      wave_lds_order();
+    }
+  }
+}
+#else
 template <int NS>
 struct RasterLds {
   RecImage<NS> img;                     // staged bin records
@@ -1321,11 +1559,23 @@ struct RasterLds {
 template <bool kCov, int NS>
 __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev& s, const BatchDev& b, RasterLds<NS>& L,
                                              uint32_t beg, uint32_t end, const uint32_t* bins, const Rec* recs,
-                                             uint32_t rec_cap) {
+                                             uint32_t rec_cap, uint32_t rfirst) {
   const int tid = threadIdx.x;
+#if CSG_PREFETCH_BIN
+  // software-pipelined staging: each batch's record ids are loaded one batch
+  // ahead (issued after the current batch's records, consumed by the next
+  // batch; the first batch's by k_raster before the z-buffer initialisation),
+  // so a batch's staging waits for one dependent load, not two
+  uint32_t rnext = rfirst;
+#endif
   for (uint32_t base = beg; base < end; base += NS) {
     uint32_t row0;
+#if CSG_PREFETCH_BIN
+    const uint32_t rows = stage_record_r<NS>(recs, rnext, rec_cap, L.img, tid, c.ox, c.oy, row0);
+    rnext = (tid < NS && base + NS + (uint32_t)tid < end) ? bins[base + NS + tid] : 0xFFFFFFFFu;
+#else
     const uint32_t rows = stage_record(recs, bins, base + tid, end, rec_cap, L.img, tid, c.ox, c.oy, row0);
+#endif
     if (tid < NS) L.row0[tid] = (uint8_t)row0;
     if constexpr (kCov) {   // label of the staged record (read back from this thread's own slot)
       if (tid < NS) {
@@ -1438,6 +1688,7 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
     }
   }
 }
+#endif  // CSG_WAVE_ROWS
 
 // ---------------------------------------------------------------------------
 // per-pixel resolve
@@ -1788,6 +2039,9 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
     empty_tile(s, b, f, tile, ox, oy);
     return;
   }
+  const uint32_t* bins = b.bins + sb.bin_base;
+  // the first batch's record ids, loaded before the z-buffer initialisation (CSG_PREFETCH_BIN)
+  const uint32_t rfirst = (CSG_PREFETCH_BIN && tid < NS && beg + (uint32_t)tid < end) ? bins[beg + tid] : 0xFFFFFFFFu;
   for (int p = tid; p < kTilePix; p += kRB) zb[p] = kEmptyKey;
   CovLds* covp = nullptr;
   int32_t* rlabel = nullptr;
@@ -1799,12 +2053,11 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
     if (tid < kCovSlots) covl.keys[tid] = kNoAlpha;
     if (tid == 0) covl.ovf = 0u;
   }
-  const uint32_t* bins = b.bins + sb.bin_base;
   const Rec* recs = b.recs + sb.rec_base;
   RasterCtx c{s.aquad, s.acls, zb, ox, oy, s.inv_near, s.inv_far, b.dbg, b.overflow, covp, rlabel,
               kCov ? b.covered + (size_t)f * b.n_labels : nullptr};
   __syncthreads();
-  raster_block<kCov, NS>(c, s, b, L.ra.r, beg, end, bins, recs, sb.rec_cap);
+  raster_block<kCov, NS>(c, s, b, L.ra.r, beg, end, bins, recs, sb.rec_cap, rfirst);
   __syncthreads();
   if constexpr (kCov) {
     // per slot: popcount of its kTilePix / 32 mask words, kTPS threads per
@@ -2429,6 +2682,44 @@ void launch_depth_vis(const float* depth, uint32_t npx, uint32_t F, const uint32
   dim3 g(vis ? (items + 255u) / 256u : 1u, F);
   if (vec) hipLaunchKernelGGL(k_depth_vis<true>, g, dim3(256), 0, st, depth, npx, F, range, lut, vis, range_out);
   else hipLaunchKernelGGL(k_depth_vis<false>, g, dim3(256), 0, st, depth, npx, F, range, lut, vis, range_out);
+}
+
+// ---------------------------------------------------------------------------
+// k_narrow_ids: a launch chain's int32 instance ids (-1 background) as
+// (id + 1) in `bytes` = 1 or 2 bytes, the host wire of csg_api.cpp's
+// host-output batches (csg_widen.h widens them back).  Ids [lo, hi) of `src`,
+// absolute indices (src and dst are the batch buffers, 16-B aligned), 4 per
+// thread: one 16-B load and one 4-B / 8-B store; ids outside [lo, hi) of a
+// thread's aligned group are left alone.  HBM-bound: 4 B read + 1-2 B written per id.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_narrow_ids(const int32_t* __restrict__ src, size_t lo, size_t hi,
+                                                     uint32_t bytes, void* __restrict__ dst) {
+  const size_t j = (lo & ~(size_t)3) + ((size_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+  if (j >= hi) return;
+  if (j >= lo && j + 4 <= hi) {
+    const v4i32 v = __builtin_nontemporal_load(reinterpret_cast<const v4i32*>(src + j));
+    if (bytes == 1) {
+      const uint32_t w = ((uint32_t)(v.x + 1) & 255u) | (((uint32_t)(v.y + 1) & 255u) << 8) |
+                         (((uint32_t)(v.z + 1) & 255u) << 16) | ((uint32_t)(v.w + 1) << 24);
+      *reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(dst) + j) = w;
+    } else {
+      const uint2 w = make_uint2(((uint32_t)(v.x + 1) & 0xFFFFu) | ((uint32_t)(v.y + 1) << 16),
+                                 ((uint32_t)(v.z + 1) & 0xFFFFu) | ((uint32_t)(v.w + 1) << 16));
+      *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dst) + j) = w;
+    }
+    return;
+  }
+  for (size_t k = j; k < j + 4 && k < hi; ++k) {
+    if (k < lo) continue;
+    if (bytes == 1) static_cast<uint8_t*>(dst)[k] = (uint8_t)(src[k] + 1);
+    else static_cast<uint16_t*>(dst)[k] = (uint16_t)(src[k] + 1);
+  }
+}
+
+void launch_narrow_ids(const int32_t* src, size_t lo, size_t hi, uint32_t bytes, void* dst, hipStream_t st) {
+  const size_t groups = (hi - (lo & ~(size_t)3) + 3) / 4;
+  if (!groups) return;
+  hipLaunchKernelGGL(k_narrow_ids, dim3((uint32_t)((groups + 255) / 256)), dim3(256), 0, st, src, lo, hi, bytes, dst);
 }
 
 }  // namespace csg

@@ -123,7 +123,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
              width: Optional[int] = None, height: Optional[int] = None, writers: int = 0,
              resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
              writer_mode: str = "thread", renderers: int = 0, object_list: str = "visible",
-             occlusion: bool = False, sink: str = "disk") -> dict:
+             occlusion: bool = False, sink: str = "disk", validate_pointcloud: bool = False,
+             min_points: int = 100, max_retries: int = 5) -> dict:
     """Render ``frames`` on one GPU and write them (``outputs``, default the
     reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
     add the depth .npy, the depth .npy + CSV, the point cloud, the normals).
@@ -142,7 +143,13 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     raster time).
     ``sink`` "discard" runs the whole pipeline (render, GPU encode, copy
     into the page-locked ring, writer threads) but writes every file to
-    /dev/null: the generator's steady-state rate without a file system."""
+    /dev/null: the generator's steady-state rate without a file system.
+    ``validate_pointcloud`` (off by default, as ``enable_pointcloud_validation``
+    in the reference, GDP:61): a frame whose point cloud has fewer than
+    ``min_points`` points (GDP:59; the GPU's count of valid depth pixels) is
+    rendered again from a jittered camera (Workload.camera's ``attempt``,
+    GDP:1573-1581), up to ``max_retries`` attempts in all (GDP:60); a frame
+    that fails them all is logged failed and writes no files (GDP:1662-1666)."""
     if object_list not in OBJECT_LISTS:
         raise ValueError(f"object_list {object_list!r}: choose from {OBJECT_LISTS}")
     outs = set(REFERENCE_OUTPUTS if outputs is None else outputs)
@@ -169,6 +176,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     host_depth = "depth_npy" in outs or (not gpu_files and bool(outs & {"depth_csv", "pointcloud"}))
     log = QualityLog(os.path.join(out_dir, "logs"))
     want = render_outputs(outs, gpu_files, host_depth, occlusion)
+    if validate_pointcloud and "depth_stats" not in want:
+        want.append("depth_stats")   # the per-frame valid point count the validation reads
     n_writers = writers or default_writers()
     # Renderer contexts on the device, each with its own stream and work
     # buffers, rendering alternate batches from their own threads: one batch's
@@ -239,20 +248,47 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
             set_of[e] = k
         views, projs = wl.frame_params(fb)
         tr = time.time()
-        fr = make_frames(views, projs, [set_of[f // 10] for f in fb], fb)
-        if kinds:
-            outs_b = {k: v[:len(fb)] for k, v in arrays.items() if k not in ("files", "file_offsets")}
-            out, offsets, need = r.render_files(fr, kinds, arrays["files"], want=want, out=outs_b)
-            if offsets is None:   # the files did not fit: a larger buffer, no re-render
-                offsets = r.copy_files(pool.grow_files(slot, need + need // 4, alloc=r.host_buffer,
-                                                       free=r.free_host_buffer), len(fb) * nk)
-            arrays["file_offsets"] = offsets
-            d2h.append(int(offsets[-1]) + sum(v.nbytes for v in out.values()))
-        else:
-            out = r.render(fr, want=want, out={k: v[:len(fb)] for k, v in arrays.items()})
-            d2h.append(sum(v.nbytes for v in out.values()))
+        sets = [set_of[f // 10] for f in fb]
+
+        def run(views, projs):
+            fr = make_frames(views, projs, sets, fb)
+            if kinds:
+                outs_b = {k: v[:len(fb)] for k, v in arrays.items() if k not in ("files", "file_offsets")}
+                out, offsets, need = r.render_files(fr, kinds, arrays["files"], want=want, out=outs_b)
+                if offsets is None:   # the files did not fit: a larger buffer, no re-render
+                    offsets = r.copy_files(pool.grow_files(slot, need + need // 4, alloc=r.host_buffer,
+                                                           free=r.free_host_buffer), len(fb) * nk)
+                arrays["file_offsets"] = offsets
+                d2h.append(int(offsets[-1]) + sum(v.nbytes for v in out.values()))
+            else:
+                out = r.render(fr, want=want, out={k: v[:len(fb)] for k, v in arrays.items()})
+                d2h.append(sum(v.nbytes for v in out.values()))
+            return out
+
+        out = run(views, projs)
+        attempts, checks, failed = [0] * len(fb), [[] for _ in fb], [False] * len(fb)
+        if validate_pointcloud:   # GDP:1573-1645: retry frames whose point cloud is too small
+            check = range(len(fb))
+            while True:
+                pts = out["depth_stats"][:len(fb), 0]
+                again = []
+                for k in check:
+                    if pts[k] >= min_points:
+                        continue
+                    checks[k].append(int(pts[k]))
+                    if attempts[k] + 1 < max_retries:
+                        attempts[k] += 1
+                        again.append(k)
+                    else:
+                        failed[k] = True
+                if not again:
+                    break
+                # the whole batch again, the retried frames from their jittered cameras (the
+                # others render exactly as before: every frame is a pure function of its pose)
+                out = run(*wl.frame_params(fb, attempts))
+                check = again
         te = time.time()
-        return fb, slot, out, (te - tr, tp - tw, tr - tp)
+        return fb, slot, out, (te - tr, tp - tw, tr - tp), attempts, checks, failed
 
     ahead = ThreadPoolExecutor(max_workers=n_rend)
     prep = ThreadPoolExecutor(max_workers=1)
@@ -268,7 +304,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         queued = [ahead.submit(render_batch, b) for b in range(min(n_rend, len(starts)))]
         for b in range(len(starts)):
             tq = time.time()
-            fb, slot, out, (dt, dwait, dprep) = queued.pop(0).result()
+            fb, slot, out, (dt, dwait, dprep), attempts, checks, failed = queued.pop(0).result()
             t_main_wait += time.time() - tq
             t_render += dt
             t_slot_wait += dwait
@@ -281,7 +317,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                 if e not in pose_cache:
                     pose_cache[e] = object_poses(wl.scene, wl.epoch(e).object_frames)
             for k, f in enumerate(fb):
-                V, P, C, cam, aim, q = wl.camera(f)
+                if failed[k]:   # every validation attempt failed: logged, nothing written (GDP:1662-1666)
+                    log.frame_failed(f, wl.camera(f)[3], checks[k])
+                    continue
+                V, P, C, cam, aim, q = wl.camera(f, attempts[k])
                 listed = (in_frustum(wl.scene, wl.epoch(f // 10).object_frames, V, P, wl.width, wl.height,
                                      intr.near, intr.far) if object_list == "frustum" else None)
                 if lw is not None:
@@ -297,7 +336,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                                        listed=listed)
                     n_obj = lab["num_objects"]
                 log_args = dict(n_objects=n_obj, kp_vis=out["keypoints_vis"][k].copy(), frame_id=f,
-                                cam_pos=cam, depth_range=out["depth_range"][k].copy() if "depth_range" in out else None)
+                                cam_pos=wl.camera(f)[3] if attempts[k] else cam, failed_checks=checks[k],
+                                depth_range=out["depth_range"][k].copy() if "depth_range" in out else None)
                 if "depth_stats" in out:   # valid, zero, inf, sum, min, max (csg_outputs.depth_stats)
                     v = out["depth_stats"][k].tolist()
                     log_args["gpu_depth_stats"] = {"valid": int(v[0]), "zero": int(v[1]), "inf": int(v[2]),
@@ -391,13 +431,19 @@ def main(argv=None):
     ap.add_argument("--no-resume", action="store_true")
     ap.add_argument("--sink", default="disk", choices=("disk", "discard"),
                     help="discard: the whole pipeline, every file written to /dev/null (steady-state measurement)")
+    ap.add_argument("--validate-pointcloud", action="store_true",
+                    help="re-render frames with fewer than --min-points points from a jittered camera "
+                         "(the reference's enable_pointcloud_validation, off by default there too)")
+    ap.add_argument("--min-points", type=int, default=100, help="point-cloud validation threshold (GDP:59)")
+    ap.add_argument("--max-retries", type=int, default=5, help="validation attempts per frame (GDP:60)")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
     summary = generate(out, frames, a.workload, a.seed, a.batch, a.device, a.depth, a.depth_csv, a.pointcloud,
                        a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
                        outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode, renderers=a.renderers,
-                       object_list=a.object_list, occlusion=a.occlusion, sink=a.sink)
+                       object_list=a.object_list, occlusion=a.occlusion, sink=a.sink,
+                       validate_pointcloud=a.validate_pointcloud, min_points=a.min_points, max_retries=a.max_retries)
     print(json.dumps(summary))
 
 

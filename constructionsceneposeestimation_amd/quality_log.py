@@ -58,15 +58,18 @@ class QualityLog:
     def frame(self, n_objects: int, depth: Optional[np.ndarray] = None, kp_vis: Optional[np.ndarray] = None,
               frame_id: Optional[int] = None, cam_pos: Optional[Sequence[float]] = None,
               depth_range: Optional[Sequence[float]] = None, points: Optional[int] = None,
-              depth_stats: Optional[dict] = None) -> dict:
+              depth_stats: Optional[dict] = None, failed_checks: Sequence[int] = ()) -> dict:
         """Record one rendered frame (the reference's log_frame_start ...
         log_frame_end sequence for a frame that succeeded).  The depth entry
         comes from ``depth_stats`` (writers.depth_stats, computed by a writer
-        thread) or from the ``depth`` array."""
+        thread) or from the ``depth`` array.  ``failed_checks``: the point
+        counts of the point-cloud validation attempts that failed before this
+        one passed (GDP:1573-1645; one retry each, log_retry :278-283)."""
         rec = {"frame_id": int(frame_id) if frame_id is not None else self.c["total_attempts"],
                "camera_position": [float(x) for x in cam_pos] if cam_pos is not None else None,
                "retry_count": 0, "status": "processing", "issues": []}
         msg = [f"\n{'=' * 60}\nframe {rec['frame_id']} start\ncamera position: {rec['camera_position']}\n"]
+        self._retries(rec, msg, failed_checks)
         self.c["total_attempts"] += 1
         self.c["successful_frames"] += 1
         self.c["rgb_success"] += 1
@@ -110,6 +113,49 @@ class QualityLog:
         self._lines.append("".join(msg))
         if len(self._lines) >= 64:
             self.flush()
+        return rec
+
+    def _retries(self, rec: dict, msg: List[str], failed_checks: Sequence[int]) -> None:
+        """The point-cloud validation's failed attempts (GDP:1626-1645): each
+        counts as an empty or insufficient point cloud, each but a last
+        failing one leads to a retry (log_retry, :278-283)."""
+        for k, n in enumerate(failed_checks):
+            n = int(n)
+            if n == 0:
+                self.stats["pointcloud_stats"]["empty"] += 1
+                rec["issues"].append("point cloud empty: no pixel hit")
+                msg.append("  - point cloud empty\n")
+            else:
+                self.stats["pointcloud_stats"]["insufficient"] += 1
+                rec["issues"].append(f"point cloud insufficient: {n} points")
+                msg.append(f"  - point cloud insufficient: {n} points\n")
+        retries = len(failed_checks)
+        rec["retry_count"] = retries
+        self.stats["retry_count"] += retries
+        for k in range(1, retries + 1):
+            msg.append(f"  ! retry {k}\n")
+
+    def frame_failed(self, frame_id: int, cam_pos: Optional[Sequence[float]], failed_checks: Sequence[int]) -> dict:
+        """A frame whose every validation attempt failed: the reference logs it
+        failed and writes nothing for it (GDP:1662-1666, log_frame_end(False)
+        :374-387).  Its attempts beyond the first were retries."""
+        rec = {"frame_id": int(frame_id), "camera_position": [float(x) for x in cam_pos] if cam_pos is not None else None,
+               "retry_count": 0, "status": "processing", "issues": []}
+        msg = [f"\n{'=' * 60}\nframe {rec['frame_id']} start\ncamera position: {rec['camera_position']}\n"]
+        self._retries(rec, msg, failed_checks)
+        # the last failed check ends the loop without a retry
+        rec["retry_count"] = max(0, len(failed_checks) - 1)
+        self.stats["retry_count"] -= 1 if failed_checks else 0
+        if failed_checks:
+            msg.pop()
+        self.c["total_attempts"] += 1
+        self.c["failed_frames"] += 1
+        self.stats["total_frames_attempted"] += 1
+        self.stats["failed_frames"] += 1
+        rec["status"] = "failed"
+        msg.append(f">>> frame {rec['frame_id']} failed\n")
+        self.frame_logs.append(rec)
+        self._lines.append("".join(msg))
         return rec
 
     def _depth(self, rec: dict, msg: List[str], ds: dict, depth_range) -> None:

@@ -324,6 +324,13 @@ class Renderer:
         self._check(self.lib.csg_instance_bounds(self.ctx, set_id, out.ctypes.data), "instance_bounds")
         return out.reshape(-1, 2, 3)
 
+    def host_id_bytes(self) -> int:
+        """Bytes per instance id on the host wire of host-output batches (1, 2 or 4; csg_host_id_bytes)."""
+        n = self.lib.csg_host_id_bytes(self.ctx)
+        if n < 0:
+            self._check(n, "host_id_bytes")
+        return int(n)
+
     def synchronize(self) -> None:
         self._check(self.lib.csg_synchronize(self.ctx), "synchronize")
 

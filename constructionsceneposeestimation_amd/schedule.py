@@ -45,12 +45,23 @@ FENCE_Y = (-9.0, 9.0)                                           # :936
 DUMPER_AREAS = [(-7, -1), (-3, -5), (5, 0), (-5, 5), (3, -4), (6, 3), (-6, -4)]   # :1110-1118
 
 STREAM_CAMERA_RING, STREAM_CAMERA_RANDOM, STREAM_LAYOUT, STREAM_POSE, STREAM_DR = 1, 2, 3, 4, 5
+STREAM_RETRY = 6
 
 
 def rng_for(seed: int, stream: int, index: int) -> np.random.Generator:
     """Counter-based stream: independent of every other (stream, index)."""
     return np.random.Generator(np.random.Philox(key=[seed & 0xFFFFFFFFFFFFFFFF,
                                                      ((stream & 0xFFFF) << 48) | (index & 0xFFFFFFFFFFFF)]))
+
+
+def retry_offset(seed: int, k: int, attempt: int) -> np.ndarray:
+    """Camera jitter of validation retry ``attempt`` (>= 1) of frame k: the
+    reference's ``np.random.uniform(-2, 2, size=3)`` with the z offset halved
+    (generate_construction_data.py:1574-1579), drawn from its own counter
+    stream keyed by (seed, frame, attempt) instead of the global NumPy state."""
+    off = rng_for(seed, STREAM_RETRY, (k << 4) | (attempt & 15)).uniform(-2.0, 2.0, size=3)
+    off[2] *= 0.5
+    return off
 
 
 def camera_pose(seed: int, k: int) -> Tuple[np.ndarray, np.ndarray]:

@@ -97,24 +97,31 @@ class Workload:
         self._cam_cache: Dict[int, tuple] = {}
 
     # -- per frame ------------------------------------------------------------
-    def camera(self, frame: int):
+    def camera(self, frame: int, attempt: int = 0):
         """(V, P, C, cam, aim, q) of a frame; memoised (the generator asks for
-        a frame's camera when it renders it and again for its label)."""
-        hit = self._cam_cache.get(frame)
+        a frame's camera when it renders it and again for its label).
+        ``attempt`` > 0: the pose of the point-cloud validation's retry
+        ``attempt`` (GDP:1573-1581): the camera moved by
+        schedule.retry_offset, still aimed at the frame's aim point -- a
+        pitched shot whenever the jitter moved it off the aim point's height."""
+        key = (frame, attempt)
+        hit = self._cam_cache.get(key)
         if hit is not None:
             return hit
         cam, aim = schedule.camera_pose(self.seed, frame)
+        if attempt:
+            cam = cam + schedule.retry_offset(self.seed, frame, attempt)
         q = cm.look_at_world_quat(cam, aim)
         V, P, C = cm.frame_matrices(cam, q, self.intr)
         if len(self._cam_cache) >= 4096:
             self._cam_cache.clear()
-        self._cam_cache[frame] = out = (V, P, C, cam, aim, q)
+        self._cam_cache[key] = out = (V, P, C, cam, aim, q)
         return out
 
-    def frame_params(self, frame_ids) -> Tuple[np.ndarray, np.ndarray]:
+    def frame_params(self, frame_ids, attempts=None) -> Tuple[np.ndarray, np.ndarray]:
         Vs, Ps = [], []
-        for k in frame_ids:
-            V, P, *_ = self.camera(int(k))
+        for j, k in enumerate(frame_ids):
+            V, P, *_ = self.camera(int(k), int(attempts[j]) if attempts is not None else 0)
             Vs.append(V)
             Ps.append(P)
         return np.stack(Vs), np.stack(Ps)

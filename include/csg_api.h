@@ -35,11 +35,15 @@
  *   csg_size_work / csg_get_work_info (per-frame work-buffer caps measured
  *                               on a sample of frames; no reference counterpart:
  *                               Kit sizes its own render buffers)
+ *   csg_host_id_bytes ......... width of the instance ids on the host wire
+ *                               (int32 mask of :1909-1910 narrowed to
+ *                               id + 1 bytes on PCIe, widened on the host)
  *   csg_last_error / csg_destroy
  *
  * Threading: several contexts may share a device (each has its own stream
  * and work buffers; the generator drives two from two threads); a context is
- * used by one thread at a time.  No global state.
+ * used by one thread at a time.  The only process-wide state is the pool of
+ * host threads that widens narrowed instance ids (csg_host_id_bytes).
  */
 #ifndef CSG_API_H
 #define CSG_API_H
@@ -67,7 +71,7 @@ typedef struct csg_ctx csg_ctx;
 
 typedef struct {
   int32_t device;            /* HIP device ordinal (after HIP_VISIBLE_DEVICES) */
-  uint32_t width, height;    /* output resolution, e.g. 1920x1080; at most 8192 x 4096 (256 x 256
+  uint32_t width, height;    /* output resolution, e.g. 1920x1080; at most 8192 x 8192 (256 x 512
                                 tiles of 32 x 16: CSG_ERR_INVALID beyond) */
   uint32_t max_frames;       /* frames per csg_render_batch call (work buffers sized for it) */
   float near_clip, far_clip; /* 0.5 / 250 m, generate_construction_data.py:1437; in [2^-126, 2^126] */
@@ -310,6 +314,15 @@ typedef struct {
 int csg_size_work(csg_ctx* ctx, csg_frame* frames, uint32_t n_frames, int32_t frames_on_device,
                   float margin, csg_work_info* out);
 int csg_get_work_info(csg_ctx* ctx, csg_work_info* out);
+
+/* Bytes per instance id on the host wire of host-output batches: 1 when every
+ * instance label is in [-1, 254], 2 up to 65,534, else 4 (int32 as rendered).
+ * The ids cross PCIe as (id + 1) in that width and are widened into the
+ * caller's int32 array on host threads (the reference's int32 mask,
+ * generate_construction_data.py:1909-1910, :2066-2069) before the batch's
+ * stream completes; CSG_NARROW_IDS=0 at csg_create keeps int32 on the wire.
+ * Returns the width (1, 2 or 4), or a negative status. */
+int csg_host_id_bytes(const csg_ctx* ctx);
 
 /* Stand-alone 3D->2D projection (host buffers): uv [n][2], vis [n] without a
  * depth test (1 = in front and inside the image, 0 otherwise). */

@@ -48,8 +48,9 @@ def test_invalid_config_rejected_without_gpu():
     assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
     bad = _lib.Config(0, 1920, 1080, 8, 0.5, 1e38, 0, 0)
     assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
-    # more than 256 x 256 tiles of 32 x 16 (8-bit tile coordinates in the tile rectangles)
-    bad = _lib.Config(0, 1920, 4097, 8, 0.5, 250.0, 0, 0)
+    # more than 256 x 512 tiles of 32 x 16 (8-bit tile coordinates in the tile rectangles, tile-row
+    # pairs above 256 rows)
+    bad = _lib.Config(0, 1920, 8193, 8, 0.5, 250.0, 0, 0)
     assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1
     bad = _lib.Config(0, 8193, 1080, 8, 0.5, 250.0, 0, 0)
     assert lib.csg_create(C.byref(bad), C.byref(ctx)) == -1

@@ -1,11 +1,14 @@
 """The largest frames the library accepts, bit-exact against the oracle.
 
 A raster record's tile rectangle packs tile coordinates in 8 bits
-(`rec_tile_rect`), so `csg_create` accepts at most 256 x 256 tiles of 32x16:
-8192 x 4096 px (`tests/test_abi.py` pins the rejection one pixel beyond).
-Here the limit itself renders: tile coordinate 255 in both axes, 65,536 tiles
-per frame (8 binning blocks per frame above 8,192 tiles), and a one-tile-row
-frame at the full width with a ragged height.  Above 32,768 tiles the binning
+(`rec_tile_rect`); frames of more than 256 tile rows store tile-row pairs, so
+`csg_create` accepts at most 256 x 512 tiles of 32x16: 8192 x 8192 px
+(`tests/test_abi.py` pins the rejection one pixel beyond).  Here the limits
+render: tile coordinate 255 in both axes (8192 x 4096, 65,536 tiles per
+frame, 8 binning blocks per frame above 8,192 tiles), 8K UHD (7680 x 4320:
+270 tile rows, so rows in pairs), a portrait frame at the full
+height (2048 x 8192: 512 tile rows) and a one-tile-row frame at the full
+width with a ragged height.  Above 32,768 tiles the binning
 kernels' per-tile LDS counters no longer fit a workgroup's 160 KiB, so they bin
 in bands of tiles (`kBinBand`): 8192 x 4096 takes two full bands, 6000 x 3000
 (188 x 188 ragged tiles) a full band and a short one.  (Round 5: before the
@@ -20,7 +23,7 @@ from tests.test_gpu_parity import _assert_same, _frames, _oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("W,H", [(8192, 4096), (6000, 3000), (8192, 11)])
+@pytest.mark.parametrize("W,H", [(8192, 4096), (7680, 4320), (2048, 8192), (6000, 3000), (8192, 11)])
 def test_largest_frame(world2, W, H):
     from constructionsceneposeestimation_amd.renderer import Renderer
     views, projs = pose_frames(WORLD2_POSES[5:6], W, H)   # a pitched view: geometry to the bottom row

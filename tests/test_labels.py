@@ -95,3 +95,52 @@ def test_quality_log_depth_mean_vs_reference_float32_mean():
     ours = ds["sum"] / ds["valid"]
     ref = float(np.mean(d[np.isfinite(d) & (d > 0)]))
     assert abs(ours - ref) <= 1e-6 * ref
+
+
+def test_retry_offsets_follow_the_reference_jitter():
+    """GDP:1574-1579: offset = uniform(-2, 2, 3), z halved; here from a counter
+    stream keyed by (seed, frame, attempt): reproducible, independent per attempt."""
+    from constructionsceneposeestimation_amd import schedule
+    offs = np.array([schedule.retry_offset(0, f, a) for f in range(200) for a in range(1, 5)])
+    assert np.abs(offs[:, :2]).max() <= 2.0 and np.abs(offs[:, 2]).max() <= 1.0
+    assert np.abs(offs[:, :2]).max() > 1.9 and np.abs(offs[:, 2]).max() > 0.9
+    assert np.array_equal(schedule.retry_offset(0, 7, 2), schedule.retry_offset(0, 7, 2))
+    assert not np.array_equal(schedule.retry_offset(0, 7, 2), schedule.retry_offset(0, 7, 3))
+    assert not np.array_equal(schedule.retry_offset(0, 7, 2), schedule.retry_offset(1, 7, 2))
+
+
+def test_retried_camera_is_jittered_and_pitched():
+    from constructionsceneposeestimation_amd import schedule
+    from constructionsceneposeestimation_amd.workload import Workload
+    wl = Workload("C3", seed=0, width=160, height=96)
+    V0, P0, C0, cam0, aim0, q0 = wl.camera(12)
+    V2, P2, C2, cam2, aim2, q2 = wl.camera(12, 2)
+    assert np.allclose(cam2, cam0 + schedule.retry_offset(0, 12, 2)) and np.array_equal(aim2, aim0)
+    assert abs(cam0[2] - aim0[2]) < 1e-12 and abs(cam2[2] - aim2[2]) > 1e-6   # level shot -> pitched
+    fwd = C2[:3, :3] @ np.array([0.0, 0.0, -1.0])                             # USD camera looks down -Z
+    d = (aim2 - cam2) / np.linalg.norm(aim2 - cam2)
+    assert np.allclose(fwd, d, atol=1e-9)
+    V, P = wl.frame_params([12, 13], attempts=[2, 0])
+    assert np.array_equal(V[0], V2) and np.array_equal(V[1], wl.camera(13)[0])
+
+
+def test_quality_log_counts_validation_retries(tmp_path):
+    """The reference's retry bookkeeping (log_retry :278-283, log_pointcloud
+    :285-300, log_frame_end :374-387): a frame that passed on its third
+    attempt has retry_count 2 and two failed point-cloud checks; one that
+    failed all five attempts is 'failed' with retry_count 4 (the fifth check
+    ends the loop without a retry)."""
+    from constructionsceneposeestimation_amd.quality_log import QualityLog
+    log = QualityLog(str(tmp_path))
+    ds = {"valid": 500, "total": 1000, "zero": 0, "inf": 500, "sum": 1000.0, "min": 1.0, "max": 3.0}
+    rec = log.frame(n_objects=2, frame_id=3, cam_pos=[0, 0, 1], depth_stats=ds, points=500, failed_checks=[0, 40])
+    assert rec["retry_count"] == 2 and rec["status"] == "success"
+    bad = log.frame_failed(4, [1, 1, 1], [0, 0, 10, 0, 5])
+    assert bad["retry_count"] == 4 and bad["status"] == "failed"
+    st = log.statistics()
+    assert st["retry_count"] == 6 and st["failed_frames"] == 1 and st["successful_frames"] == 1
+    assert st["total_frames_attempted"] == 2
+    assert st["pointcloud_stats"] == {"valid": 1, "empty": 4, "insufficient": 3}
+    log.save()
+    text = open(tmp_path / "generation_detail.log").read()
+    assert text.count("! retry") == 6 and "frame 4 failed" in text

@@ -11,7 +11,7 @@ src=constructionsceneposeestimation_amd/csrc
 tmp=$(mktemp -d)
 mkdir -p $tmp/pkg/csrc $tmp/include
 cp include/csg_api.h $tmp/include/
-cp $src/csg_api.cpp $src/csg_kernels.hip $src/csg_kernels.h $src/csg_encode.hip $src/csg_encode.h $src/csg_deflate.h $tmp/pkg/csrc/
+cp $src/csg_api.cpp $src/csg_kernels.hip $src/csg_kernels.h $src/csg_encode.hip $src/csg_encode.h $src/csg_deflate.h $src/csg_widen.h $tmp/pkg/csrc/
 if [ "$rev" != "-" ]; then
   for f in csg_kernels.hip csg_kernels.h; do git show $rev:$src/$f > $tmp/pkg/csrc/$f; done
 fi

@@ -15,6 +15,9 @@ from collections import defaultdict
 N_CU = 256
 N_SIMD = N_CU * 4   # MI355X: 256 CUs x 4 SIMDs
 N_XCD = 8
+# VALU pipe occupancy that 8 waves per SIMD of independent v_fma_f32 reach on the MI355X
+# (k_fma_indep<8>, profiles/r06/calib/summary.json): the practical ceiling for a kernel
+VALU_PIPE_CEILING = 0.80
 
 
 def _grid(row):
@@ -61,13 +64,26 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
     for k, o in out.items():
         if "FETCH_SIZE" in o and "WRITE_SIZE" in o:
             o["hbm_bytes_per_launch"] = o["FETCH_SIZE"] * 1024 * 2 + o["WRITE_SIZE"] * 1024
-        if "SQ_ACTIVE_INST_VALU" in o and "GRBM_GUI_ACTIVE" in o and o["GRBM_GUI_ACTIVE"] > 0:
-            # VALU issue utilisation: SQ_ACTIVE_INST_VALU counts quad-cycles (one wave64 VALU
-            # instruction = one quad-cycle of its SIMD), summed over the chip's 1,024 SIMDs;
-            # GRBM_GUI_ACTIVE is summed over the 8 XCDs
-            o["valu_busy"] = o["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / (o["GRBM_GUI_ACTIVE"] / N_XCD)
-            if "SQ_THREAD_CYCLES_VALU" in o and o["SQ_ACTIVE_INST_VALU"] > 0:
+        if "GRBM_GUI_ACTIVE" in o and o["GRBM_GUI_ACTIVE"] > 0:
+            cyc = o["GRBM_GUI_ACTIVE"] / N_XCD   # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+            # VALU pipe occupancy, calibrated on gfx950 (tools/calib_valu.hip, profiles/r06/calib):
+            # SQ_ACTIVE_INST_VALU counts ONE per wave64 VALU instruction (= SQ_INSTS_VALU, at 1 and
+            # at 8 waves per SIMD alike), and a SIMD-32 pipe takes 2 cycles per wave64 instruction
+            # (MI355X_MICROARCH.md:54, :473); 8 waves per SIMD of independent v_fma_f32 reach 0.80.
+            # (Round 5's formula, SQ_ACTIVE_INST_VALU x 4 / SIMDs / cycles, is twice this and
+            # exceeded 1.)
+            n_valu = o.get("SQ_INSTS_VALU", o.get("SQ_ACTIVE_INST_VALU"))
+            if n_valu is not None:
+                o["valu_pipe_occupancy"] = n_valu * 2 / N_SIMD / cyc
+            if "SQ_THREAD_CYCLES_VALU" in o and o.get("SQ_ACTIVE_INST_VALU", 0) > 0:
                 o["valu_lane_util"] = o["SQ_THREAD_CYCLES_VALU"] / (o["SQ_ACTIVE_INST_VALU"] * 64)
+            if o.get("SQ_WAVE_CYCLES"):
+                # wave-cycles: parked on s_waitcnt / s_barrier (SQ_WAIT_ANY), stalled with an
+                # instruction ready (SQ_WAIT_INST_ANY), issuing (SQ_ACTIVE_INST_ANY); disjoint
+                wc = o["SQ_WAVE_CYCLES"]
+                o["wave_cycles"] = {k: round(o[c] / wc, 4) for k, c in (("parked", "SQ_WAIT_ANY"),
+                                    ("issue_stall", "SQ_WAIT_INST_ANY"), ("issuing", "SQ_ACTIVE_INST_ANY")) if c in o}
+                o["waves_per_simd"] = wc * 4 / N_SIMD / cyc   # SQ_WAVE_CYCLES in quad-cycles
         if "SQ_LDS_IDX_ACTIVE" in o and o["SQ_LDS_IDX_ACTIVE"] > 0:
             # LDS-array cycles (summed over the 256 CUs) and the extra cycles bank conflicts
             # added to them (MI355X_MICROARCH.md §LDS): conflict share and LDS busy per CU
@@ -100,7 +116,9 @@ def main(root, write_profile=False, workload="C3", frames_per_launch=60):
                               "MI355X_MICROARCH.md §HBM), WRITE_SIZE x1; KB = 1024 B. Basis for k_raster's access "
                               "mix: profiles/r01/fetch_calibration.json (4-B gathers and 112-B records also cost "
                               "one 128-B request per touched line)",
-                "k_raster_valu_busy": out["k_raster"].get("valu_busy"),
+                "k_raster_valu_pipe_occupancy": out["k_raster"].get("valu_pipe_occupancy"),
+                "valu_pipe_ceiling": VALU_PIPE_CEILING,
+                "k_raster_wave_cycles": out["k_raster"].get("wave_cycles"),
                 "k_raster_valu_lane_util": out["k_raster"].get("valu_lane_util"),
                 "source": os.path.basename(os.path.normpath(root))}
         path = os.path.join(here, "profiles", "pmc_traffic.json")
