@@ -18,7 +18,8 @@ LIB = os.path.join(PKG, "libcsg.so")
 SOURCES = [os.path.join(PKG, "csrc", "csg_kernels.hip"), os.path.join(PKG, "csrc", "csg_encode.hip"),
            os.path.join(PKG, "csrc", "csg_api.cpp")]
 DEPS = SOURCES + [os.path.join(PKG, "csrc", "csg_kernels.h"), os.path.join(PKG, "csrc", "csg_encode.h"),
-                  os.path.join(PKG, "csrc", "csg_deflate.h"), os.path.join(ROOT, "include", "csg_api.h")]
+                  os.path.join(PKG, "csrc", "csg_deflate.h"), os.path.join(PKG, "csrc", "csg_widen.h"),
+                  os.path.join(ROOT, "include", "csg_api.h")]
 ARCH = os.environ.get("CSG_OFFLOAD_ARCH", "gfx950")
 IO_LIB = os.path.join(PKG, "libcsgio.so")
 IO_SOURCES = [os.path.join(PKG, "csrc", "csg_io.cpp")]
@@ -31,7 +32,7 @@ JSON_SOURCES = [os.path.join(PKG, "csrc", "csg_json.cpp"), os.path.join(PKG, "cs
 # -ffp-contract=off: the raster spec's float expressions must round exactly as
 # written (bit-exact with the CPU oracle).  HIP keeps fp32 '/' and sqrtf
 # correctly rounded by default; do not add -ffast-math.
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}", "-Wall"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}", "-Wall", "-pthread"]
 
 
 def hipcc() -> str:

@@ -11,7 +11,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <numeric>
 #include <cstddef>
 #include <cmath>
 #include <cstdarg>
@@ -1069,13 +1068,6 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
       HIP_TRY(c, hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming));
     }
   }
-  // k_raster's 4-pixel vector stores test alignment relative to the chain's
-  // first pixel: chains start at pixel c0 * npx, a multiple of 4 when G is a
-  // multiple of 4 / gcd(npx, 4) (F = G frames otherwise)
-  {
-    const uint32_t m = 4u / (uint32_t)std::gcd<size_t>(npx, 4);
-    if (G < F) G = std::min(F, (G + m - 1) / m * m);
-  }
   std::shared_ptr<WidenLatch> latch;
   if (narrow) {
     const size_t nb = (size_t)F * npx * c->ids_bytes;
@@ -1097,6 +1089,9 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     const uint32_t Fc = std::min(G, F - c0);
     BatchDev bc = b;
     bc.frames = dframes + c0;
+    // k_raster's 4-pixel vector stores test the alignment of the absolute pixel
+    // index: the chain starts at pixel c0 * npx of the batch's buffers
+    bc.px_align = (uint32_t)(((size_t)c0 * npx) & 3u);
     if (bc.rgb) bc.rgb += (size_t)c0 * npx * 3;
     if (bc.inst) bc.inst += (size_t)c0 * npx;
     if (bc.depth) bc.depth += (size_t)c0 * npx;

@@ -190,6 +190,7 @@ struct BatchDev {
   uint32_t* drange;            // [2][drange_F] min / max bits of the valid depths of each frame, reduced by
   uint32_t drange_F;           //   k_raster's resolve (null: not wanted)
   uint32_t dbg;                // ablation switches for profiling only (CSG_DEBUG env; 0 in production)
+  uint32_t px_align;           // (first pixel of this launch chain in the output buffers) mod 4
 };
 
 // launchers (all enqueue on `st`)

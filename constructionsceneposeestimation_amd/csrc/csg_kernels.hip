@@ -1989,7 +1989,7 @@ __device__ __forceinline__ void empty_tile(const SceneDev& s, const BatchDev& b,
   const size_t o = (size_t)f * s.W * s.H + (size_t)py * s.W + px0;
   const uint32_t sky = b.lights[b.fset[f]].sky & 0xFFFFFFu;
   const float nan = __builtin_nanf("");
-  if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
+  if (px0 + 3 < (int)s.W && ((o + b.px_align) & 3u) == 0) {
     if (b.inst) out_ids(b.inst + o, make_int4(-1, -1, -1, -1));
     if (b.rgb) out_rgb4(b.rgb + o * 3, sky, sky, sky, sky);
     if (b.depth) out_f4(b.depth + o, INFINITY, INFINITY, INFINITY, INFINITY);
@@ -2262,7 +2262,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
       // pixel strides: at 4K those narrow stores were 30% of k_raster).
       // (o % 4 == 0 keeps the group's outputs 16-B aligned, as in empty_tile.)
       bool vec = false;
-      if (CSG_VEC_OUT && (b.depth || b.normals || b.points) && inmask == 0xFu && (qo & 3u) == 0) {
+      if (CSG_VEC_OUT && (b.depth || b.normals || b.points) && inmask == 0xFu && ((qo + b.px_align) & 3u) == 0) {
         uint32_t done = first ? bgmask : 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) done |= ((slots >> (8 * k)) & 0xFFu) != 0xFFu ? 1u << k : 0u;
@@ -2376,7 +2376,7 @@ __global__ __launch_bounds__(kRasterBlock) CSG_RASTER_ATTR void k_raster(SceneDe
       rgb[k] = (uint32_t)w;
       ids[k] = (int32_t)(w >> 32);
     }
-    if (px0 + 3 < (int)s.W && (o & 3u) == 0) {
+    if (px0 + 3 < (int)s.W && ((o + b.px_align) & 3u) == 0) {
       if (b.inst) out_ids(b.inst + o, make_int4(ids[0], ids[1], ids[2], ids[3]));
       if (b.rgb) out_rgb4(b.rgb + o * 3, rgb[0], rgb[1], rgb[2], rgb[3]);
     } else {

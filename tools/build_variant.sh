@@ -15,7 +15,7 @@ cp $src/csg_api.cpp $src/csg_kernels.hip $src/csg_kernels.h $src/csg_encode.hip 
 if [ "$rev" != "-" ]; then
   for f in csg_kernels.hip csg_kernels.h; do git show $rev:$src/$f > $tmp/pkg/csrc/$f; done
 fi
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared -ffp-contract=off --offload-arch=gfx950 -Wall "$@" \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared -ffp-contract=off --offload-arch=gfx950 -Wall -pthread "$@" \
   -o constructionsceneposeestimation_amd/libcsg_$name.so $tmp/pkg/csrc/csg_kernels.hip $tmp/pkg/csrc/csg_encode.hip $tmp/pkg/csrc/csg_api.cpp
 rm -rf $tmp
 echo built constructionsceneposeestimation_amd/libcsg_$name.so
