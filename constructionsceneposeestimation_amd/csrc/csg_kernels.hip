@@ -1046,31 +1046,6 @@ __device__ __forceinline__ void row_span(const uint4& g0, const uint4& g1, int o
   }
 }
 
-#ifndef CSG_WR_DEBUG
-#define CSG_WR_DEBUG 0   // debug builds only: check every span end and fragment with the exact edge test
-#endif
-// The spec's exact coverage of tile pixel (lx, ly) by a staged record (int64, as row_span<false>).
-__device__ __forceinline__ bool exact_cover(const uint4& g0, const uint4& g1, int ox, int oy, int lx, int ly) {
-  const int32_t RX[3] = {(int32_t)g0.x, (int32_t)g0.y, (int32_t)g0.z};
-  const int32_t RY[3] = {(int32_t)g0.w, (int32_t)g1.x, (int32_t)g1.y};
-  const int64_t cx = (int64_t)(ox + lx) * 256 + 128, cy = (int64_t)(oy + ly) * 256 + 128;
-  const int ea[3] = {1, 2, 0}, eb[3] = {2, 0, 1};
-  bool in = true;
-  for (int e = 0; e < 3; ++e) {
-    const int64_t ax = RX[ea[e]], ay = RY[ea[e]], dx = (int64_t)RX[eb[e]] - ax, dy = (int64_t)RY[eb[e]] - ay;
-    const int bias = (dy < 0 || (dy == 0 && dx > 0)) ? 0 : -1;
-    in &= dx * (cy - ay) - dy * (cx - ax) + bias >= 0;
-  }
-  return in;
-}
-__device__ __forceinline__ void wr_debug_report(uint32_t* ov, uint32_t what, uint32_t a, uint32_t b2, uint32_t c2,
-                                                uint32_t d, uint32_t e) {
-  atomicAdd(&ov[what], 1u);
-  if (atomicCAS(&ov[7], 0u, what) == 0u) {
-    ov[8] = a; ov[9] = b2; ov[10] = c2; ov[11] = d; ov[12] = e;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // k_raster: one 32x32 tile of one frame per 256-thread workgroup
 // ---------------------------------------------------------------------------
@@ -1109,7 +1084,7 @@ static_assert(kStage <= kRasterBlock && CSG_COV_STAGE <= kRasterBlock, "one stag
 constexpr int kRB = kRasterBlock;
 // level-2 items of one level-1 round: up to kRB spans of up to kTileW pixels,
 // as 32-item words of the start bitmap
-[[maybe_unused]] constexpr int kL2Words = kRB * kTileW / 32;
+constexpr int kL2Words = kRB * kTileW / 32;
 constexpr int kColWords = (kTileW + 31) / 32;   // 32-bit column masks per tile row (label statistics)
 template <bool kCov>
 constexpr int kStageOf = kCov ? CSG_COV_STAGE : kStage;
@@ -1344,198 +1319,19 @@ __device__ __forceinline__ uint32_t stage_record_r(const Rec* recs, uint32_t r, 
   return y0 <= y1 ? (uint32_t)(y1 - y0 + 1) : 0u;
 }
 
-// Wave-private rows (CSG_WAVE_ROWS, round 6): after the one barrier that ends
-// a batch's staging, wave w of the workgroup owns the tile rows ly = w (mod
-// kNW) -- interleaved, so a batch's rows split evenly -- and runs level 1
-// and level 2 of those rows alone: its (record, row) items, its spans and its
-// fragments, with wave-level DPP scans and its own bookkeeping in LDS.  No
-// other wave reads or writes its z-buffer rows or its bookkeeping, so there is
-// no s_barrier until the next batch is staged (the block-wide version crosses
-// two per batch and three per level-1 round).  Lanes of one wave see each
-// other's LDS writes in program order (the LDS executes a wave's instructions
-// in order); wave_lds_order() only keeps the compiler from moving accesses
-// across those hand-offs.
-#ifndef CSG_WAVE_ROWS
-#define CSG_WAVE_ROWS 0
-#endif
+// Software-pipelined staging (round 6): a batch's bin entries (record ids)
+// are loaded one batch ahead -- the first batch's by k_raster before the
+// z-buffer initialisation, each later batch's right after the previous batch's
+// records -- so a batch's staging waits for one dependent global load (the
+// record) instead of two (bin entry, then record).  Staging was 92% parked
+// wave-cycles.  Measured on C3 at 2,880 frames per launch, 3 runs
+// each: k_raster 96.4 -> 93.8 ms, frames/s +2.3%, 72 VGPRs either way
+// (profiles/r06/ab/raster_variants_F2880.txt).  CSG_PREFETCH_BIN=0 builds the
+// previous staging for A/B.
 #ifndef CSG_PREFETCH_BIN
-#define CSG_PREFETCH_BIN 0     // A/B: the block version's record ids one batch ahead
+#define CSG_PREFETCH_BIN 1
 #endif
-constexpr int kNW = kRB / 64;                      // waves per raster workgroup
-constexpr int kRowsW = kTileH / kNW;               // tile rows each wave owns
-static_assert((kNW & (kNW - 1)) == 0 && kTileH % kNW == 0, "rows split evenly over the waves");
-#ifndef CSG_WAVE_ORDER_WAIT
-#define CSG_WAVE_ORDER_WAIT 0
-#endif
-__device__ __forceinline__ void wave_lds_order() {
-  if (CSG_WAVE_ORDER_WAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-// exclusive wave64 scan; `total` = the wave's sum (lane 63's inclusive value)
-#ifndef CSG_WR_HALVES
-#define CSG_WR_HALVES 0    // A/B: wave w owns rows [w * kRowsW, (w + 1) * kRowsW) instead of ly = w (mod kNW)
-#endif
-#ifndef CSG_WR_SHFL
-#define CSG_WR_SHFL 0
-#endif
-#ifndef CSG_WR_CHECK
-#define CSG_WR_CHECK 0
-#endif
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total, uint32_t* flag = nullptr) {
-  const uint32_t inc = wave_incl_scan(v);
-  total = CSG_WR_SHFL ? (uint32_t)__shfl((int)inc, 63, 64) : (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-  if (CSG_WR_CHECK && flag) {
-    const uint32_t t2 = (uint32_t)__shfl((int)inc, 63, 64);
-    if (t2 != total && (threadIdx.x & 63) == 0) atomicOr(flag, 64u);
-  }
-  return inc - v;
-}
-// one wave's level-1 / level-2 bookkeeping (NS <= 64 staged records: one per lane)
-template <int NS>
-struct WaveLds {
-  static constexpr int kW1 = (NS * kRowsW + 31) / 32;   // level-1 item words (<= NS * kRowsW items)
-  static constexpr int kW2 = 64 * kTileW / 32;          // level-2 item words (<= 64 spans of <= kTileW px)
-  uint32_t crec[NS];          // compact record: slot | first item << 8 | first row << 18 | small << 23
-  uint32_t span[64];          // rec | ly << 8 | (ex2 - xl + kTileW) << 16
-  uint32_t starts1[kW1];      // bit i: a record's rows start at level-1 item i
-  uint32_t starts[kW2];       // bit i: a span starts at level-2 item i
-  uint8_t before1[kW1 + 1];   // records starting before item 32*d (<= NS <= 64)
-  uint8_t before[kW2 + 1];    // spans starting before item 32*d (<= 64)
-};
 
-#if CSG_WAVE_ROWS
-template <int NS>
-struct RasterLds {
-  static_assert(NS <= 64, "wave-private rows: one staged record per lane");
-  RecImage<NS> img;                     // staged bin records
-  uint16_t rinfo[NS];                   // first tile row | 0x80 if small | row count << 8
-  WaveLds<NS> w[kNW];
-};
-
-template <bool kCov, int NS>
-__device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev& s, const BatchDev& b, RasterLds<NS>& L,
-                                             uint32_t beg, uint32_t end, const uint32_t* bins, const Rec* recs,
-                                             uint32_t rec_cap, uint32_t) {
-  const int tid = threadIdx.x;
-  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
-  WaveLds<NS>& V = L.w[wv];
-  for (uint32_t base = beg; base < end; base += NS) {
-    if (base != beg) __syncthreads();   // every wave is done with the previous batch's image
-    uint32_t row0;
-    const uint32_t rows = stage_record(recs, bins, base + tid, end, rec_cap, L.img, tid, c.ox, c.oy, row0);
-    if (tid < NS) L.rinfo[tid] = (uint16_t)(row0 | (rows << 8));
-    if constexpr (kCov) {   // label of the staged record (read back from this thread's own slot)
-      if (tid < NS) {
-        int32_t lab = -1;
-        if (rows) {
-          lab = s.inst[L.img.q[2][tid].x >> s.uid_shift].label;
-          if (lab >= 0 && (uint32_t)lab >= b.n_labels) lab = -1;
-        }
-        c.rlabel[tid] = lab;
-      }
-    }
-    if ((DBG(b.dbg) & 512u) && rows) {   // profiling counters: records with rows in the tile, row items
-      atomicAdd(&b.overflow[1], 1u);
-      atomicAdd(&b.overflow[2], rows);
-    }
-    __syncthreads();
-    // this wave's rows of record `lane`: ly = wv (mod kNW) inside [a, a + n)
-    uint32_t cnt = 0, fr = 0, sm = 0;
-    if (lane < (uint32_t)NS) {
-      const uint32_t ri = L.rinfo[lane], a = ri & 31u, n = ri >> 8;
-      sm = (ri >> 7) & 1u;
-#if CSG_WR_HALVES
-      fr = max(a, wv * (uint32_t)kRowsW);
-      const uint32_t last = min(a + n, (wv + 1u) * (uint32_t)kRowsW);
-      cnt = n && fr < last ? last - fr : 0u;
-#else
-      fr = a + ((wv - a) & (uint32_t)(kNW - 1));
-      cnt = fr < a + n ? (a + n - 1u - fr) / (uint32_t)kNW + 1u : 0u;
-#endif
-    }
-    if (lane < (uint32_t)WaveLds<NS>::kW1) V.starts1[lane] = 0u;
-    if (lane == 0) V.before1[0] = 0;
-    uint32_t tot1p;
-    const uint32_t ex1p = wave_excl_scan(cnt | (cnt ? 0x10000u : 0u), tot1p, b.overflow);
-    const uint32_t tot1 = tot1p & 0xFFFFu;
-    wave_lds_order();
-    if (cnt) {
-      const uint32_t ex1 = ex1p & 0xFFFFu, ci = ex1p >> 16, e_end = ex1 + cnt;
-      V.crec[ci] = lane | (ex1 << 8) | (fr << 18) | (sm << 23);
-      atomicOr(&V.starts1[ex1 >> 5], 1u << (ex1 & 31u));
-      if ((e_end & ~31u) > ex1) V.before1[e_end >> 5] = (uint8_t)(ci + 1u);   // cnt <= kRowsW <= 32
-    }
-    wave_lds_order();
-    for (uint32_t c1 = 0; c1 < ((DBG(b.dbg) & 256u) ? 0u : tot1); c1 += 64u) {
-      const uint32_t j1 = c1 + lane;
-      uint32_t w2 = 0, sp = 0;
-      int xl = 0;
-      if (j1 < tot1) {
-        const uint32_t w1 = V.starts1[j1 >> 5], nb1 = V.before1[j1 >> 5];
-        const uint32_t cr = V.crec[nb1 + (uint32_t)__popc(w1 & (0xFFFFFFFFu >> (31u - (j1 & 31u)))) - 1u];
-        const int k = (int)(cr & 255u);
-        const uint32_t first = (cr >> 8) & 1023u;
-        const uint4 g0 = L.img.q[0][k], g1 = L.img.q[1][k];
-        const int x0 = max((int)(g1.z & 0xFFFFu) - c.ox, 0), x1 = min((int)(g1.w & 0xFFFFu) - c.ox, kTileW - 1);
-        const int ly = (int)((cr >> 18) & 31u) + (CSG_WR_HALVES ? 1 : kNW) * (int)(j1 - first);
-        int xr;
-        if (DBG(b.dbg) & 1024u) { xl = 1; xr = 0; }   // ablation: no span computation
-        else if (cr & (1u << 23)) row_span<true>(g0, g1, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
-        else {
-          if (DBG(b.dbg) & 512u) atomicAdd(&b.overflow[8], 1u);   // profiling: row items on the int64 path
-          row_span<false>(g0, g1, c.ox, c.oy, ly, x0, x1, xl, xr, DBG(b.dbg) & 2048u);
-        }
-        if (xl <= xr) {
-          w2 = (uint32_t)(xr - xl + 1);
-          sp = (uint32_t)k | ((uint32_t)ly << 8);
-          if (CSG_WR_DEBUG && (!exact_cover(g0, g1, c.ox, c.oy, xl, ly) || !exact_cover(g0, g1, c.ox, c.oy, xr, ly)))
-            wr_debug_report(b.overflow, 1u, (uint32_t)c.ox | ((uint32_t)c.oy << 16), (uint32_t)k | (wv << 8) | (cr & 0x800000u),
-                            (uint32_t)ly | ((uint32_t)xl << 8) | ((uint32_t)xr << 16), j1 | (first << 16), g1.z);
-        }
-      }
-      if ((DBG(b.dbg) & 512u) && w2) {      // non-empty spans, level-2 items
-        atomicAdd(&b.overflow[3], 1u);
-        atomicAdd(&b.overflow[4], w2);
-      }
-      // the chunk's non-empty spans: compact index and item offset from one
-      // packed wave scan; item -> span by a rank query (as the block version)
-#pragma unroll
-      for (int w = 0; w < WaveLds<NS>::kW2; w += 64) V.starts[w + (int)lane] = 0u;
-      if (lane == 0) V.before[0] = 0;
-      uint32_t totp;
-      const uint32_t exp = wave_excl_scan(w2 | (w2 ? 0x10000u : 0u), totp, b.overflow);
-      const uint32_t ex2 = exp & 0xFFFFu, tot2 = totp & 0xFFFFu;
-      wave_lds_order();
-      if (w2) {
-        const uint32_t ci = exp >> 16, e_end = ex2 + w2;
-        V.span[ci] = sp | ((ex2 - (uint32_t)xl + (uint32_t)kTileW) << 16);
-        atomicOr(&V.starts[ex2 >> 5], 1u << (ex2 & 31u));
-        if constexpr (kTileW <= 32) {
-          if ((e_end & ~31u) > ex2) V.before[e_end >> 5] = (uint8_t)(ci + 1u);
-        } else {
-          for (uint32_t d = (ex2 >> 5) + 1u; d <= (e_end >> 5); ++d) V.before[d] = (uint8_t)(ci + 1u);
-        }
-      }
-      wave_lds_order();
-      for (uint32_t j = lane; j < ((DBG(b.dbg) & 8u) ? 0u : tot2); j += 64u) {
-        const uint32_t w = V.starts[j >> 5], nb = V.before[j >> 5];
-        const uint32_t rank = nb + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31u - (j & 31u))));
-        const uint32_t spj = V.span[rank - 1u];
-        if (CSG_WR_DEBUG) {
-          const int kk = (int)(spj & 255u), lx = (int)(j + (uint32_t)kTileW - (spj >> 16)), ly = (int)((spj >> 8) & 255u);
-          if (lx < 0 || lx >= kTileW || !exact_cover(L.img.q[0][kk], L.img.q[1][kk], c.ox, c.oy, lx, ly))
-            wr_debug_report(b.overflow, 2u, (uint32_t)c.ox | ((uint32_t)c.oy << 16), (uint32_t)kk | (wv << 8),
-                            (uint32_t)ly | ((uint32_t)(lx & 255) << 8), j | (rank << 16), tot2);
-        }
-        fragment<kCov>(c, L.img, (int)(spj & 255u), (int)(j + (uint32_t)kTileW - (spj >> 16)), (int)((spj >> 8) & 255u));
-      }
-      wave_lds_order();
-    }
-  }
-}
-#else
 template <int NS>
 struct RasterLds {
   RecImage<NS> img;                     // staged bin records
@@ -1688,7 +1484,6 @@ __device__ __forceinline__ void raster_block(const RasterCtx& c, const SceneDev&
     }
   }
 }
-#endif  // CSG_WAVE_ROWS
 
 // ---------------------------------------------------------------------------
 // per-pixel resolve

@@ -84,6 +84,24 @@ def test_bench_two_ranks_plain_command(tmp_path):
     assert all(x["device_count"] == ndev for x in sh["devices"])
     assert sh["shared_devices"] is (ndev < 2)
     assert sh["distinct_devices"] == min(2, ndev)
+    # each rank's own timing (round 6): elapsed seconds, frames/s, stage times;
+    # the slowest rank sets ms_per_step, and the imbalance is max/min elapsed
+    prs = sh["per_rank"]
+    assert [x["rank"] for x in prs] == [0, 1]
+    for x in prs:
+        assert x["elapsed_s"] > 0 and x["frames_per_s"] > 0
+        assert set(x["stage_ms_per_step"]) == {"ms_setup", "ms_bin", "ms_raster", "ms_keypoints"}
+        assert all(v >= 0 for v in x["stage_ms_per_step"].values())
+    el = [x["elapsed_s"] for x in prs]
+    assert sh["slowest_rank"] == el.index(max(el))
+    assert abs(sh["imbalance"] - max(el) / min(el)) <= 1e-3 * sh["imbalance"]
+    assert abs(d["ms_per_step"] - max(el) / steps * 1e3) <= 0.01 * d["ms_per_step"]
+    # the host-delivery leg on every rank at once
+    pc = d["pcie_inclusive"]
+    assert pc is not None and pc["ranks"] == 2 and pc["value"] > 0
+    assert [x["rank"] for x in pc["per_rank"]] == [0, 1]
+    assert all(x["frames"] > 0 and x["frames_per_s"] > 0 for x in pc["per_rank"])
+    assert pc["ids_wire_bytes"] == 1
 
 
 @pytest.mark.timeout(600)

@@ -72,6 +72,7 @@ def test_narrow_wire_matches_int32_wire_and_device_outputs(tmp_path):
         wide = b.render(fb, want=want)                      # int32 on the wire (pageable)
         narrow = a.render(fa, want=want)                     # narrowed (pageable: one chain)
         pin = a.render(fa, want=want, out=_pinned_out(a, n, want))   # narrowed, page-locked: chains overlap
+        pin = {k: v.copy() for k, v in pin.items()}   # (the page-locked buffers are freed with the renderer)
         # the device-output path (no wire at all)
         dev = torch.device("cuda", 0)
         fdev = torch.from_numpy(fa.view(np.uint8).copy()).to(dev)

@@ -125,6 +125,37 @@ def test_ragged_size_overflow_growth_and_empty_frame(world2):
     assert (gpu["instance"][2] == -1).all() and np.isinf(gpu["depth"][2]).all()
 
 
+def test_ragged_size_page_locked_chains(world2):
+    """with page-locked host outputs a batch runs as several launch
+    chains (copies overlap later chains), and at a frame size whose pixel
+    count is odd the chains start at pixel offsets that are not multiples of
+    4: the 4-pixel vector stores must test the absolute alignment.  264 frames
+    of 203x117 (8 chains of 33: the second starts at pixel 783,783) with every
+    per-pixel output, against one chain into pageable arrays and against the
+    oracle."""
+    from constructionsceneposeestimation_amd.renderer import Renderer
+    W, H = 203, 117
+    n = 264
+    poses = [WORLD2_POSES[k % len(WORLD2_POSES)] for k in range(n)]
+    views, projs = pose_frames(poses, W, H)
+    fr = _frames(views, projs)
+    want = ("rgb", "instance", "depth", "normals", "points")
+    with Renderer(world2, W, H, max_frames=n, records_per_frame=65536, bins_per_frame=131072) as r:
+        ref = r.render(fr, want=want)                      # pageable: one chain
+        pin = {}
+        for k, (shape, dt) in r.output_spec(n, want).items():
+            pin[k] = r.host_buffer(int(np.prod(shape)) * np.dtype(dt).itemsize).view(dt).reshape(shape)
+        got = r.render(fr, want=want, out=pin)             # page-locked: chains of 33 frames
+        got = {k: v.copy() for k, v in got.items()}
+    for key, a in ref.items():
+        assert np.array_equal(a.view(np.uint8), got[key].view(np.uint8)), key
+    o = _oracle(world2, W, H)
+    for f in (32, 33, 70, 263):   # chains 2, 3 and 8 start at odd pixel offsets
+        ora = o.render(views[f], projs[f], extra=True)
+        _assert_same(got, ora, f)
+        _assert_extra(got, ora, f)
+
+
 def _assert_extra(gpu, ora, f):
     gn, on = gpu["normals"][f].view(np.uint16), ora["normals"].view(np.uint16)
     assert np.array_equal(gn, on), f"frame {f}: normals differ at {np.argwhere((gn != on).any(-1))[:5].tolist()}"
