@@ -208,6 +208,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
 
     t_render = t_slot_wait = t_prep = t_main_wait = t_labels = 0.0
     d2h = []   # bytes each batch copied to the host (files + arrays), appended by the render threads
+    ids_wire = r.host_id_bytes()   # instance ids cross PCIe as 1-, 2- or 4-byte values (csg_host_id_bytes)
+
+    def wire_bytes(out):   # the host arrays' bytes as they crossed PCIe (ids narrowed, widened on the host)
+        return sum(v.nbytes for v in out.values()) - (out["instance"].size * (4 - ids_wire) if "instance" in out else 0)
     t0 = time.time()
     starts = list(range(0, len(frames), batch))
 
@@ -259,10 +263,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                     offsets = r.copy_files(pool.grow_files(slot, need + need // 4, alloc=r.host_buffer,
                                                            free=r.free_host_buffer), len(fb) * nk)
                 arrays["file_offsets"] = offsets
-                d2h.append(int(offsets[-1]) + sum(v.nbytes for v in out.values()))
+                d2h.append(int(offsets[-1]) + wire_bytes(out))
             else:
                 out = r.render(fr, want=want, out={k: v[:len(fb)] for k, v in arrays.items()})
-                d2h.append(sum(v.nbytes for v in out.values()))
+                d2h.append(wire_bytes(out))
             return out
 
         out = run(views, projs)
@@ -394,6 +398,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                              "writer_task_s": round(pool.task_s, 3), "teardown_s": round(t_teardown, 3),
                              "d2h_bytes": int(sum(d2h)), "d2h_bytes_per_frame": round(sum(d2h) / max(len(frames), 1)),
                              "d2h_gbs": round(sum(d2h) / wall / 1e9, 2) if wall > 0 else None,
+                             "ids_wire_bytes": ids_wire,
                              "render_busy": round(t_render / (wall * n_rend), 3) if wall > 0 else None,
                              "sink": sink,
                              "writer_busy": round(pool.task_s / (wall * n_writers), 3) if wall > 0 else None,

@@ -84,6 +84,7 @@ def main():
                "frames_per_s": tp["frames_per_s"], "wall_s": tp["wall_s"], "seconds_incl_setup": round(dt, 2),
                "successful": s["counters"]["successful_frames"],
                "d2h_bytes_per_frame": tp["d2h_bytes_per_frame"], "d2h_gbs": tp["d2h_gbs"],
+               "ids_wire_bytes": tp.get("ids_wire_bytes"),
                "render_busy": tp["render_busy"], "renderers": tp["renderers"],
                "render_thread": tp["render_thread"], "main_thread": tp["main_thread"],
                "writers": tp["writers"], "writer_busy": tp["writer_busy"], "writer_task_s": tp["writer_task_s"],
