@@ -212,6 +212,7 @@ struct csg_ctx {
   // CSG_NARROW_IDS=0 keeps int32 on the wire (A/B, tests).
   uint32_t ids_bytes = 4;               // set by csg_upload_scene from the label range
   bool narrow_ids = true;
+  bool split_pageable = false;          // CSG_SPLIT_PAGEABLE=1: copy chains for pageable outputs too (A/B only)
   DevBuf<uint8_t> o_ids_n;              // [F][H][W] narrowed ids (device)
   uint8_t* h_ids_n = nullptr;           // ... their pinned host landing buffer
   size_t h_ids_n_bytes = 0;
@@ -317,6 +318,7 @@ int csg_create(const csg_config* cfg, csg_ctx** out) {
   c->cfg = *cfg;
   if (const char* d = getenv("CSG_DEBUG")) c->dbg = (uint32_t)strtoul(d, nullptr, 0);
   if (const char* v = getenv("CSG_NARROW_IDS")) c->narrow_ids = atoi(v) != 0;
+  if (const char* v = getenv("CSG_SPLIT_PAGEABLE")) c->split_pageable = atoi(v) != 0;
   c->chain_frames = cfg->frames_per_launch ? cfg->frames_per_launch : kAutoChainFrames;
   if (const char* v = getenv("CSG_CHAIN")) c->chain_frames = (uint32_t)std::max(1, atoi(v));
   c->chain_frames = std::min(c->chain_frames, cfg->max_frames);
@@ -1061,7 +1063,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
                           out->inst_stats, out->label_covered, out->depth_vis, out->depth_range, out->depth_stats,
                           want_kp ? out->keypoints_uv : nullptr, want_kp ? out->keypoints_vis : nullptr};
     for (const void* d : dsts) pinned = pinned && (!d || host_pinned(d));
-    if (pinned) G = std::min(G, std::max(kMinCopyChain, (F + kCopyChunks - 1) / kCopyChunks));
+    if (pinned || c->split_pageable) G = std::min(G, std::max(kMinCopyChain, (F + kCopyChunks - 1) / kCopyChunks));
     if (!c->copy_stream) {
       HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
       for (auto& e : c->copy_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));

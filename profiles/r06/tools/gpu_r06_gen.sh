@@ -18,6 +18,9 @@ timeout -k 10 400 python3 -u tools/gen_steady.py --frames $N --outputs reference
 cat $O/steady_reference.json
 timeout -k 10 300 python3 -u tools/gen_steady.py --frames ${SHM_FRAMES:-2000} --outputs $NO_PC --sink disk --dir /dev/shm > $O/shm_no_pointcloud.json 2> $O/shm_no_pointcloud.err || { tail -20 $O/shm_no_pointcloud.err; exit 1; }
 cat $O/shm_no_pointcloud.json
+# launch-chain splitting for pageable host outputs, A/B
+timeout -k 10 300 python3 -u tools/pageable_ab.py --frames 480 > $O/pageable_ab.json 2> $O/pageable_ab.err || { tail -20 $O/pageable_ab.err; exit 1; }
+cat $O/pageable_ab.json
 if [ "${N2:-1}" = 1 ]; then
   # the N = 2 line as `bench.py --gpus 2` prints it (two ranks sharing the box's one GPU)
   timeout -k 10 600 python3 bench.py --gpus 2 > $O/bench_C3_n2.json 2> $O/bench_C3_n2.err || { tail -20 $O/bench_C3_n2.err; exit 1; }
