@@ -8,8 +8,8 @@ scene of test_gpu_parity.test_many_labels_stats takes that path against the
 oracle), and host threads widen them into the caller's int32 array before the
 batch's stream completes.  Here: the widened ids equal the int32 wire's
 (CSG_NARROW_IDS=0) and the device-output path's, byte for byte, for pageable
-and page-locked host arrays, one launch chain and several, synchronous and
-asynchronous batches; and the `.npy` the generator writes from them is
+and page-locked host arrays, one launch chain and several (CSG_SPLIT_PAGEABLE),
+synchronous and asynchronous batches; and the `.npy` the generator writes from them is
 byte-identical to the one written from the int32 path.
 """
 import os
@@ -25,17 +25,20 @@ def _workload():
     return Workload("C3", seed=3, width=480, height=272)
 
 
-def _renderer(wl, n, narrow):
+def _renderer(wl, n, narrow, split_pageable=True):
+    """A renderer whose context reads CSG_NARROW_IDS / CSG_SPLIT_PAGEABLE at create."""
     from constructionsceneposeestimation_amd.renderer import Renderer
-    old = os.environ.get("CSG_NARROW_IDS")
-    os.environ["CSG_NARROW_IDS"] = "1" if narrow else "0"
+    env = {"CSG_NARROW_IDS": "1" if narrow else "0", "CSG_SPLIT_PAGEABLE": "1" if split_pageable else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         r = Renderer(wl.scene, wl.width, wl.height, max_frames=n)
     finally:
-        if old is None:
-            del os.environ["CSG_NARROW_IDS"]
-        else:
-            os.environ["CSG_NARROW_IDS"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     return r
 
 
@@ -65,12 +68,14 @@ def test_narrow_wire_matches_int32_wire_and_device_outputs(tmp_path):
     fids = list(range(0, 400, 5))   # 80 frames: with page-locked outputs, launch chains of 32, 32, 16
     n, H, W = len(fids), wl.height, wl.width
     want = ("rgb", "instance", "keypoints")
-    with _renderer(wl, n, True) as a, _renderer(wl, n, False) as b:
-        assert a.host_id_bytes() == 1, "C3's labels fit one byte"
+    with _renderer(wl, n, True) as a, _renderer(wl, n, False, split_pageable=False) as b, \
+            _renderer(wl, n, True, split_pageable=False) as c:
+        assert a.host_id_bytes() == 1 and c.host_id_bytes() == 1, "C3's labels fit one byte"
         assert b.host_id_bytes() == 4
-        fa, fb = _setup(a, wl, fids), _setup(b, wl, fids)
-        wide = b.render(fb, want=want)                      # int32 on the wire (pageable)
-        narrow = a.render(fa, want=want)                     # narrowed (pageable: one chain)
+        fa, fb, fc = _setup(a, wl, fids), _setup(b, wl, fids), _setup(c, wl, fids)
+        wide = b.render(fb, want=want)                      # int32 on the wire (pageable, one chain)
+        narrow = a.render(fa, want=want)                     # narrowed (pageable: chains of 32, 32, 16)
+        narrow1 = c.render(fc, want=want)                    # narrowed (pageable, one chain)
         pin = a.render(fa, want=want, out=_pinned_out(a, n, want))   # narrowed, page-locked: chains overlap
         pin = {k: v.copy() for k, v in pin.items()}   # (the page-locked buffers are freed with the renderer)
         # the device-output path (no wire at all)
@@ -92,7 +97,7 @@ def test_narrow_wire_matches_int32_wire_and_device_outputs(tmp_path):
         a._check(a.lib.csg_render_batch_async(a.ctx, fa.ctypes.data, n, 0, C.byref(o), None), "async")
         a.synchronize()
         async_inst = a_inst.copy()
-    for got in (narrow, pin):
+    for got in (narrow, narrow1, pin):
         assert got["instance"].dtype == np.int32
         assert np.array_equal(got["instance"], wide["instance"])
         assert np.array_equal(got["rgb"], wide["rgb"])

@@ -1,11 +1,11 @@
 """A/B of launch-chain splitting for pageable host outputs.
 
 Renderer.render with the default pageable numpy outputs (RGB8, int32 ids,
-keypoints), C3 1080p, one batch of F frames: as shipped (one launch chain:
-pageable destinations are not split) against CSG_SPLIT_PAGEABLE=1 (chains of
-F/8 frames, each copied while the next would render -- but a pageable copy
-blocks the host).  And the same batch into page-locked outputs, where the
-split is on.  Median of 5 after one warm-up; prints one JSON line.
+keypoints), C3 1080p, one batch of F frames: one launch chain
+(CSG_SPLIT_PAGEABLE=0) against chains of F/8 frames (the default since this
+A/B: a pageable copy blocks the host, so later chains do not render under it,
+but each chain's narrowed ids are widened while the next chain copies).  And
+the same batch into page-locked outputs.  Median of 5 after one warm-up; prints one JSON line.
 
     python tools/pageable_ab.py --frames 480
 """
