@@ -491,6 +491,27 @@ __device__ __forceinline__ uint32_t rect_tile(uint32_t rc, uint32_t q, uint32_t 
 }
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+// Chunk cull of one (frame, chunk): true if all 8 corners of the chunk's
+// object-space AABB fail one frustum plane by a margin -- then every triangle
+// inside would fail that plane in the per-triangle test too, so the output is
+// unchanged.  Corner c of the box (x from bit 2, y bit 1, z bit 0).  (Measured:
+// per-64-triangle slice AABBs cull more but cost more than they save.)
+struct CullOut { bool n, f, l, r, t, b; };
+__device__ __forceinline__ CullOut corner_out(const SceneDev& s, const Chunk& ch, const float* Cm, int c) {
+  const float px = (c & 4) ? ch.hi[0] : ch.lo[0];
+  const float py = (c & 2) ? ch.hi[1] : ch.lo[1];
+  const float pz = (c & 1) ? ch.hi[2] : ch.lo[2];
+  const float X = dot4(Cm + 0, px, py, pz), Y = dot4(Cm + 4, px, py, pz), Wc = dot4(Cm + 8, px, py, pz);
+  const float tol = 1e-3f * (fabsf(X) + fabsf(Y) + fabsf(Wc)) + 1e-3f;
+  return CullOut{Wc < s.near_clip - tol, Wc > s.far_clip + tol, X < -tol, X > (float)s.W * Wc + tol * (float)s.W,
+                 Y < -tol, Y > (float)s.H * Wc + tol * (float)s.H};
+}
+
+// The records of one chunk of triangles for frame f (one triangle per thread
+// of a 256-thread block; `sw` is the calling wave's record stage).
+__device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b, const Chunk& ch, uint32_t f,
+                                            int tid, int lane, uint4* sw);
+
 // Grid: x = frame (fast), (y, z) = chunk.  Consecutive workgroups take the
 // same chunk for successive frames, so a chunk's triangles (and its clip
 // rows' instance) are read from HBM once and then hit in L2 (measured on C3:
@@ -502,33 +523,66 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   const int tid = threadIdx.x, lane = tid & 63;
   if (DBG(b.dbg) & 32u) return;            // ablation: empty setup
   const Chunk& ch = chunks[chunk];   // read fields in place (a runtime-indexed copy would spill)
-  const uint32_t i = ch.inst;
-  const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
-  // Chunk cull: every wave evaluates the 8 corners of the chunk's object-space
-  // AABB (lanes 0-7) and the block leaves if all corners fail one frustum
-  // plane by a margin -- then every triangle inside would fail that plane in
-  // the per-triangle test too, so the output is unchanged.  (Measured: per-
-  // 64-triangle slice AABBs cull more but cost more than they save.)
+  // every wave evaluates the 8 corners (lanes 0-7); the block leaves together
   {
-    bool out_n = true, out_f = true, out_l = true, out_r = true, out_t = true, out_b = true;
-    const int cidx = lane & 7;
-    const float px = (cidx & 4) ? ch.hi[0] : ch.lo[0];
-    const float py = (cidx & 2) ? ch.hi[1] : ch.lo[1];
-    const float pz = (cidx & 1) ? ch.hi[2] : ch.lo[2];
-    const float X = dot4(Cm + 0, px, py, pz), Y = dot4(Cm + 4, px, py, pz), Wc = dot4(Cm + 8, px, py, pz);
-    const float tol = 1e-3f * (fabsf(X) + fabsf(Y) + fabsf(Wc)) + 1e-3f;
-    out_n = Wc < s.near_clip - tol;
-    out_f = Wc > s.far_clip + tol;
-    out_l = X < -tol;
-    out_r = X > (float)s.W * Wc + tol * (float)s.W;
-    out_t = Y < -tol;
-    out_b = Y > (float)s.H * Wc + tol * (float)s.H;
+    const CullOut o = corner_out(s, ch, b.clip + ((size_t)f * s.n_inst + ch.inst) * 12, lane & 7);
     const uint64_t m8 = 0xFFull;
-    const bool cull = ((__ballot(out_n) & m8) == m8) || ((__ballot(out_f) & m8) == m8) ||
-                      ((__ballot(out_l) & m8) == m8) || ((__ballot(out_r) & m8) == m8) ||
-                      ((__ballot(out_t) & m8) == m8) || ((__ballot(out_b) & m8) == m8);
+    const bool cull = ((__ballot(o.n) & m8) == m8) || ((__ballot(o.f) & m8) == m8) ||
+                      ((__ballot(o.l) & m8) == m8) || ((__ballot(o.r) & m8) == m8) ||
+                      ((__ballot(o.t) & m8) == m8) || ((__ballot(o.b) & m8) == m8);
     if (cull || (DBG(b.dbg) & 64u)) return;   // identical in every wave of the block (64: ablation, cull all)
   }
+  static_assert(16 * kRecGroups <= 2 * 64, "two chunk stores per lane");
+  __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
+  setup_chunk(s, b, ch, f, tid, lane, tstage[tid >> 6]);
+}
+
+// CSG_SETUP_LIST (A/B): the chunk cull as its own kernel, one thread per
+// (frame, chunk), writing a live flag per slot chunk * F + frame; then a
+// persistent k_setup_list (a grid that fills the GPU once) walks the slots in
+// blocks of 64 (block j on workgroup j mod grid), each wave loading the 64
+// flags at once and running the live slots.  No workgroup is dispatched for a
+// culled chunk, and none at all per (frame, chunk): 9.8 M dispatches per C3
+// launch of 2,880 frames become ~1.5 k.
+#ifndef CSG_SETUP_LIST
+#define CSG_SETUP_LIST 0
+#endif
+__global__ __launch_bounds__(256) void k_cull(SceneDev s, BatchDev b, const Chunk* __restrict__ chunks,
+                                              uint32_t n_chunks, uint32_t F, uint8_t* __restrict__ live) {
+  const uint32_t f = blockIdx.x * 256u + threadIdx.x, chunk = blockIdx.y + blockIdx.z * gridDim.y;
+  if (f >= F || chunk >= n_chunks) return;
+  const Chunk& ch = chunks[chunk];
+  const float* Cm = b.clip + ((size_t)f * s.n_inst + ch.inst) * 12;
+  bool n = true, fa = true, l = true, r = true, t = true, bo = true;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const CullOut o = corner_out(s, ch, Cm, c);
+    n &= o.n; fa &= o.f; l &= o.l; r &= o.r; t &= o.t; bo &= o.b;
+  }
+  live[(size_t)chunk * F + f] = (n | fa | l | r | t | bo) ? 0u : 1u;
+}
+
+__global__ __launch_bounds__(256) void k_setup_list(SceneDev s, BatchDev b, const Chunk* __restrict__ chunks,
+                                                    uint32_t F, uint32_t n_slots, const uint8_t* __restrict__ live) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
+  const uint32_t nblk = (n_slots + 63u) / 64u;
+  for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // uniform bounds: every wave exits
+    const uint32_t sl = blk * 64u + (uint32_t)lane;
+    uint64_t m = __ballot(sl < n_slots && live[sl] != 0);
+    while (m) {
+      const uint32_t k = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+      m &= m - 1ull;
+      const uint32_t slot = blk * 64u + k, chunk = slot / F;
+      setup_chunk(s, b, chunks[chunk], slot - chunk * F, tid, lane, tstage[tid >> 6]);
+    }
+  }
+}
+
+__device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b, const Chunk& ch, uint32_t f,
+                                            int tid, int lane, uint4* sw) {
+  const uint32_t i = ch.inst;
+  const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
 
   // Records: groups 0-1 per sub-triangle (r0, r1: named, never runtime-
   // indexed, which would put them in scratch), groups 2-4 shared (the
@@ -668,9 +722,6 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   // -1.1%, profiles/r03/ab/nt_record_stores.txt; round 1's non-temporal stores
   // of scattered 112-B records were 5x slower: partial lines).
   // Wave-local: the loop count is uniform per wave, so there is no block barrier.
-  static_assert(16 * kRecGroups <= 2 * 64, "two chunk stores per lane");
-  __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
-  uint4* sw = tstage[tid >> 6];
   const uint64_t rbase = b.slab[f].rec_base;
   const uint32_t rcap = b.slab[f].rec_cap;
   if (lane == 0 && wbase + wtot > rcap) atomicOr(b.overflow, 1u);
@@ -2405,9 +2456,27 @@ void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t s
   hipLaunchKernelGGL(k_clip, g, dim3(256), 0, st, s, b);
 }
 
+bool setup_uses_list() { return CSG_SETUP_LIST != 0; }
+
 void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks, uint32_t F,
-                  hipStream_t st) {
+                  uint8_t* live, hipStream_t st) {
   const uint32_t gy = n_chunks < 65535u ? n_chunks : 65535u;   // grid y limit
+  if (CSG_SETUP_LIST && live) {
+    hipLaunchKernelGGL(k_cull, dim3((F + 255u) / 256u, gy, (n_chunks + gy - 1) / gy), dim3(256), 0, st, s, b, chunks,
+                       n_chunks, F, live);
+    static int grid = 0;   // resident workgroups of k_setup_list on the device (one wave of the grid)
+    if (!grid) {
+      int dev = 0, cus = 0, per_cu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_setup_list, kBlock, 0);
+      grid = std::max(1, cus * std::max(1, per_cu));
+    }
+    const uint32_t n_slots = n_chunks * F;
+    const uint32_t g = std::min<uint32_t>((uint32_t)grid, (n_slots + 63u) / 64u);
+    hipLaunchKernelGGL(k_setup_list, dim3(g), dim3(kBlock), 0, st, s, b, chunks, F, n_slots, live);
+    return;
+  }
   dim3 g(F, gy, (n_chunks + gy - 1) / gy);
   hipLaunchKernelGGL(k_setup, g, dim3(kBlock), 0, st, s, b, chunks, n_chunks);
 }
