@@ -214,7 +214,6 @@ struct csg_ctx {
   bool narrow_ids = true;
   bool split_pageable = true;           // CSG_SPLIT_PAGEABLE=0: pageable host outputs as one chain (A/B, tests)
   DevBuf<uint8_t> o_ids_n;              // [F][H][W] narrowed ids (device)
-  DevBuf<uint8_t> setup_live;           // [chunks][F] chunk-cull flags (CSG_SETUP_LIST builds only)
   uint8_t* h_ids_n = nullptr;           // ... their pinned host landing buffer
   size_t h_ids_n_bytes = 0;
   // the last sizing pass (csg_size_work)
@@ -1130,8 +1129,7 @@ static int enqueue_batch(csg_ctx* c, const csg_frame* frames, uint32_t F, int fr
     launch_plan(bc.frames, Fc, c->rec_cap, (c->bin_cap + 3u) & ~3u, c->rec_pool, c->bin_pool, c->use_hints ? 1 : 0,
                 c->slab.p, c->plan_need.p, st);
     launch_clip(s, bc, Fc, st);
-    if (setup_uses_list()) HIP_TRY(c, c->setup_live.alloc((size_t)c->n_chunks * G));
-    launch_setup(s, bc, c->chunks.p, c->n_chunks, Fc, c->setup_live.p, st);
+    launch_setup(s, bc, c->chunks.p, c->n_chunks, Fc, st);
     if (c->timing) HIP_TRY(c, hipEventRecord(c->ev[1], st));
     launch_count(s, bc, Fc, c->bin_blocks, st);
     launch_colscan(s, bc, Fc, st);   // k_count's grid -> block offsets and tile counts
@@ -1530,8 +1528,7 @@ static int measure_work(csg_ctx* c, const csg_frame* frames, uint32_t n, bool on
       launch_plan(df, Fc, cap, 0x7FFFFFFCu, (uint64_t)P * cap, (uint64_t)P * 0x7FFFFFFCull, 0, c->slab.p,
                   c->plan_need.p, st);
       launch_clip(s, b, Fc, st);
-      if (setup_uses_list()) HIP_TRY(c, c->setup_live.alloc((size_t)c->n_chunks * Fc));
-      launch_setup(s, b, c->chunks.p, c->n_chunks, Fc, c->setup_live.p, st);
+      launch_setup(s, b, c->chunks.p, c->n_chunks, Fc, st);
       launch_count(s, b, Fc, c->bin_blocks, st);
       launch_colscan(s, b, Fc, st);
       launch_scan(s, b, Fc, st);

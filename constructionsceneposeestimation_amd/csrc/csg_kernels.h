@@ -208,10 +208,8 @@ inline uint32_t hinted_cap(uint32_t count, double margin, uint32_t pad) {
   return (uint32_t)(((v < 0x7FFFFFF0ull ? v : 0x7FFFFFF0ull) + 3u) & ~3ull);
 }
 void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
-// live: F x n_chunks bytes of scratch for the CSG_SETUP_LIST build (setup_uses_list()), else unused
-bool setup_uses_list();
 void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks,
-                  uint32_t F, uint8_t* live, hipStream_t st);
+                  uint32_t F, hipStream_t st);
 void launch_count(const SceneDev& s, const BatchDev& b, uint32_t F, uint32_t blocks, hipStream_t st);
 void launch_scan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);
 void launch_colscan(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t st);

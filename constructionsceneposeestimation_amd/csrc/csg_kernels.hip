@@ -537,48 +537,6 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   setup_chunk(s, b, ch, f, tid, lane, tstage[tid >> 6]);
 }
 
-// CSG_SETUP_LIST (A/B): the chunk cull as its own kernel, one thread per
-// (frame, chunk), writing a live flag per slot chunk * F + frame; then a
-// persistent k_setup_list (a grid that fills the GPU once) walks the slots in
-// blocks of 64 (block j on workgroup j mod grid), each wave loading the 64
-// flags at once and running the live slots.  No workgroup is dispatched for a
-// culled chunk, and none at all per (frame, chunk): 9.8 M dispatches per C3
-// launch of 2,880 frames become ~1.5 k.
-#ifndef CSG_SETUP_LIST
-#define CSG_SETUP_LIST 0
-#endif
-__global__ __launch_bounds__(256) void k_cull(SceneDev s, BatchDev b, const Chunk* __restrict__ chunks,
-                                              uint32_t n_chunks, uint32_t F, uint8_t* __restrict__ live) {
-  const uint32_t f = blockIdx.x * 256u + threadIdx.x, chunk = blockIdx.y + blockIdx.z * gridDim.y;
-  if (f >= F || chunk >= n_chunks) return;
-  const Chunk& ch = chunks[chunk];
-  const float* Cm = b.clip + ((size_t)f * s.n_inst + ch.inst) * 12;
-  bool n = true, fa = true, l = true, r = true, t = true, bo = true;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const CullOut o = corner_out(s, ch, Cm, c);
-    n &= o.n; fa &= o.f; l &= o.l; r &= o.r; t &= o.t; bo &= o.b;
-  }
-  live[(size_t)chunk * F + f] = (n | fa | l | r | t | bo) ? 0u : 1u;
-}
-
-__global__ __launch_bounds__(256) void k_setup_list(SceneDev s, BatchDev b, const Chunk* __restrict__ chunks,
-                                                    uint32_t F, uint32_t n_slots, const uint8_t* __restrict__ live) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
-  const uint32_t nblk = (n_slots + 63u) / 64u;
-  for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // uniform bounds: every wave exits
-    const uint32_t sl = blk * 64u + (uint32_t)lane;
-    uint64_t m = __ballot(sl < n_slots && live[sl] != 0);
-    while (m) {
-      const uint32_t k = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-      m &= m - 1ull;
-      const uint32_t slot = blk * 64u + k, chunk = slot / F;
-      setup_chunk(s, b, chunks[chunk], slot - chunk * F, tid, lane, tstage[tid >> 6]);
-    }
-  }
-}
-
 __device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b, const Chunk& ch, uint32_t f,
                                             int tid, int lane, uint4* sw) {
   const uint32_t i = ch.inst;
@@ -2456,27 +2414,9 @@ void launch_clip(const SceneDev& s, const BatchDev& b, uint32_t F, hipStream_t s
   hipLaunchKernelGGL(k_clip, g, dim3(256), 0, st, s, b);
 }
 
-bool setup_uses_list() { return CSG_SETUP_LIST != 0; }
-
 void launch_setup(const SceneDev& s, const BatchDev& b, const Chunk* chunks, uint32_t n_chunks, uint32_t F,
-                  uint8_t* live, hipStream_t st) {
+                  hipStream_t st) {
   const uint32_t gy = n_chunks < 65535u ? n_chunks : 65535u;   // grid y limit
-  if (CSG_SETUP_LIST && live) {
-    hipLaunchKernelGGL(k_cull, dim3((F + 255u) / 256u, gy, (n_chunks + gy - 1) / gy), dim3(256), 0, st, s, b, chunks,
-                       n_chunks, F, live);
-    static int grid = 0;   // resident workgroups of k_setup_list on the device (one wave of the grid)
-    if (!grid) {
-      int dev = 0, cus = 0, per_cu = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_setup_list, kBlock, 0);
-      grid = std::max(1, cus * std::max(1, per_cu));
-    }
-    const uint32_t n_slots = n_chunks * F;
-    const uint32_t g = std::min<uint32_t>((uint32_t)grid, (n_slots + 63u) / 64u);
-    hipLaunchKernelGGL(k_setup_list, dim3(g), dim3(kBlock), 0, st, s, b, chunks, F, n_slots, live);
-    return;
-  }
   dim3 g(F, gy, (n_chunks + gy - 1) / gy);
   hipLaunchKernelGGL(k_setup, g, dim3(kBlock), 0, st, s, b, chunks, n_chunks);
 }
