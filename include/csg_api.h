@@ -217,7 +217,10 @@ int csg_set_dr_textures(csg_ctx* ctx, uint32_t set_id, const int32_t* texture_pe
  * the device counters and the batch rendered again, up to 6 attempts; the
  * results do not depend on the caps.  An overflow left by an earlier
  * asynchronous batch is reported first (CSG_ERR_OVERFLOW), as by
- * csg_synchronize. */
+ * csg_synchronize.  With host outputs the batch runs as launch chains of an
+ * eighth of it (at least 32 frames), each chain's outputs copied to the host
+ * on a copy stream while later chains render (CSG_SPLIT_PAGEABLE=0 at
+ * csg_create: pageable destinations as one chain). */
 int csg_render_batch(csg_ctx* ctx, const csg_frame* frames, uint32_t n_frames, const csg_outputs* out);
 /* Same, enqueued on `stream` (a hipStream_t, NULL = context stream); frames
  * may be a device pointer when frames_on_device = 1.  Returns after enqueue;
