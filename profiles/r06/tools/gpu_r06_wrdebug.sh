@@ -1,4 +1,9 @@
 #!/bin/bash
+# Round 6 (historical): the wave-private rows variant's parity debug -- world2
+# 1080p through the variant builds (wrwait, blk) against the oracle
+# (wr_debug.py).  The variant was rejected and its code removed from the
+# kernels (archived in ../ab/wave_rows_raster_block.hip.txt), so this script
+# only documents what was run.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 O=gpurun_out/r06/wrdebug
