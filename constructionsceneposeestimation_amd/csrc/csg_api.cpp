@@ -359,6 +359,9 @@ void csg_destroy(csg_ctx* c) {
   if (!c) return;
   if (c->last_stream && c->last_stream != c->stream) (void)hipStreamSynchronize(c->last_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  // (every batch's stream waits for its copies and id widening on the copy
+  // stream, copy_done; synchronized here too before the buffers they read go)
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->set_mats.release(); c->iset.release(); c->lights.release();
   c->chunks.release();
   c->texels.release();
@@ -378,7 +381,6 @@ void csg_destroy(csg_ctx* c) {
   }
   for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
-  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);   // (widening included: see enqueue_batch)
   if (c->h_ids_n) (void)hipHostFree(c->h_ids_n);
   c->o_ids_n.release();
   for (auto& e : c->copy_ev)
