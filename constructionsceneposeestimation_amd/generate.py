@@ -37,13 +37,15 @@ import json
 import os
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
+import multiprocessing as mp
+from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
 from functools import partial
 from typing import List, Optional
 
 import numpy as np
 
 from . import camera_math as cm
+from . import prep_pool
 from .labels import OBJECT_LISTS, in_frustum, label_record, object_poses
 from .quality_log import QualityLog
 from .renderer import Renderer, make_frames, output_spec, scene_labels
@@ -124,7 +126,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
              resume: bool = True, normals: bool = False, outputs: Optional[tuple] = None,
              writer_mode: str = "thread", renderers: int = 0, object_list: str = "visible",
              occlusion: bool = False, sink: str = "disk", validate_pointcloud: bool = False,
-             min_points: int = 100, max_retries: int = 5) -> dict:
+             min_points: int = 100, max_retries: int = 5, prep_workers: int = -1) -> dict:
     """Render ``frames`` on one GPU and write them (``outputs``, default the
     reference's set; ``depth`` / ``depth_csv`` / ``pointcloud`` / ``normals``
     add the depth .npy, the depth .npy + CSV, the point cloud, the normals).
@@ -149,7 +151,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     ``min_points`` points (GDP:59; the GPU's count of valid depth pixels) is
     rendered again from a jittered camera (Workload.camera's ``attempt``,
     GDP:1573-1581), up to ``max_retries`` attempts in all (GDP:60); a frame
-    that fails them all is logged failed and writes no files (GDP:1662-1666)."""
+    that fails them all is logged failed and writes no files (GDP:1662-1666).
+    ``prep_workers``: processes that prepare batches ahead (epoch layouts,
+    object poses, cameras; prep_pool.py), so that numpy work does not hold
+    this process's GIL; -1 = two for runs of at least 20 batches, else none."""
     if object_list not in OBJECT_LISTS:
         raise ValueError(f"object_list {object_list!r}: choose from {OBJECT_LISTS}")
     outs = set(REFERENCE_OUTPUTS if outputs is None else outputs)
@@ -166,6 +171,15 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         os.makedirs(os.path.join(out_dir, d), exist_ok=True)
     if resume:
         frames = [f for f in frames if not os.path.exists(os.path.join(out_dir, "labels", f"label_{f:06d}.json"))]
+    # batch preparation in worker processes, started (like the writer processes
+    # below) before this process touches the GPU; each builds its own Workload
+    n_prep = prep_workers if prep_workers >= 0 else (2 if len(frames) >= 20 * batch else 0)
+    ppool = None
+    if n_prep:
+        ppool = ProcessPoolExecutor(max_workers=n_prep, mp_context=mp.get_context("spawn"),
+                                    initializer=prep_pool.init, initargs=(workload, seed, width, height))
+        for f in [ppool.submit(prep_pool.ping) for _ in range(2 * n_prep)]:   # every worker started now
+            f.result()
     # Thread writers (the default): the PNGs, the depth CSV and the point
     # cloud are encoded on the GPU (Renderer.render_files, csg_encode.hip) and
     # the host only writes bytes; writer processes encode on the host (libcsgio).
@@ -219,6 +233,17 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         """Host state of batch b (epoch layouts, object poses, cameras), made
         ahead in its own thread so the render thread only renders."""
         fb = frames[starts[b]:starts[b] + batch]
+        if ppool is not None:   # computed in a worker process, installed here
+            eps, cams = ppool.submit(prep_pool.prepare, list(fb), sorted({f // 10 for f in fb})).result()
+            for e, (st, poses) in eps.items():
+                wl.install_epoch(e, st)
+                if e not in pose_cache:
+                    if len(pose_cache) >= 256:
+                        pose_cache.pop(next(iter(pose_cache)))
+                    pose_cache[e] = poses
+            for f, cam in cams.items():
+                wl.install_camera(f, cam)
+            return
         for e in sorted({f // 10 for f in fb}):
             st = wl.epoch(e)
             if e not in pose_cache:
@@ -295,7 +320,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
         return fb, slot, out, (te - tr, tp - tw, tr - tp), attempts, checks, failed
 
     ahead = ThreadPoolExecutor(max_workers=n_rend)
-    prep = ThreadPoolExecutor(max_workers=1)
+    prep = ThreadPoolExecutor(max_workers=max(1, n_prep))
     prep_f: List = []
     kPrepAhead = 3
 
@@ -381,6 +406,8 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     finally:
         ahead.shutdown(wait=True)
         prep.shutdown(wait=True)
+        if ppool is not None:
+            ppool.shutdown(wait=True, cancel_futures=True)
         pool.close()
         t_close = time.time()
         for x in rends:
@@ -400,7 +427,7 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
                              "d2h_gbs": round(sum(d2h) / wall / 1e9, 2) if wall > 0 else None,
                              "ids_wire_bytes": ids_wire,
                              "render_busy": round(t_render / (wall * n_rend), 3) if wall > 0 else None,
-                             "sink": sink,
+                             "sink": sink, "prep_workers": n_prep,
                              "writer_busy": round(pool.task_s / (wall * n_writers), 3) if wall > 0 else None,
                              "outputs": sorted(outs)}
     return summary
@@ -441,6 +468,8 @@ def main(argv=None):
                          "(the reference's enable_pointcloud_validation, off by default there too)")
     ap.add_argument("--min-points", type=int, default=100, help="point-cloud validation threshold (GDP:59)")
     ap.add_argument("--max-retries", type=int, default=5, help="validation attempts per frame (GDP:60)")
+    ap.add_argument("--prep-workers", type=int, default=-1,
+                    help="processes preparing batches ahead (-1: two for runs of >= 20 batches)")
     a = ap.parse_args(argv)
     frames = shard_of_range(a.rank, a.world, a.frames)
     out = os.path.join(a.out, f"shard_{a.rank:02d}") if a.world > 1 else a.out
@@ -448,7 +477,8 @@ def main(argv=None):
                        a.width, a.height, writers=a.writers, resume=not a.no_resume, normals=a.normals,
                        outputs=parse_outputs(a.outputs), writer_mode=a.writer_mode, renderers=a.renderers,
                        object_list=a.object_list, occlusion=a.occlusion, sink=a.sink,
-                       validate_pointcloud=a.validate_pointcloud, min_points=a.min_points, max_retries=a.max_retries)
+                       validate_pointcloud=a.validate_pointcloud, min_points=a.min_points, max_retries=a.max_retries,
+                       prep_workers=a.prep_workers)
     print(json.dumps(summary))
 
 

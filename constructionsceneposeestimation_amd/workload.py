@@ -118,6 +118,13 @@ class Workload:
         self._cam_cache[key] = out = (V, P, C, cam, aim, q)
         return out
 
+    def install_camera(self, frame: int, cam: tuple) -> None:
+        """A frame's attempt-0 camera computed elsewhere (prep_pool: the same
+        Workload arguments in a worker process give the same numbers)."""
+        if len(self._cam_cache) >= 4096:
+            self._cam_cache.clear()
+        self._cam_cache[(frame, 0)] = cam
+
     def frame_params(self, frame_ids, attempts=None) -> Tuple[np.ndarray, np.ndarray]:
         Vs, Ps = [], []
         for j, k in enumerate(frame_ids):
@@ -154,6 +161,14 @@ class Workload:
             self._epoch_cache.pop(next(iter(self._epoch_cache)))
         self._epoch_cache[e] = st
         return st
+
+    def install_epoch(self, e: int, st: EpochState) -> None:
+        """An epoch's state computed elsewhere (prep_pool)."""
+        if e in self._epoch_cache:
+            return
+        if len(self._epoch_cache) >= 256:
+            self._epoch_cache.pop(next(iter(self._epoch_cache)))
+        self._epoch_cache[e] = st
 
     def n_keypoints(self) -> int:
         return len(self.kp_table)

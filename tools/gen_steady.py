@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--sink", default="discard", choices=("disk", "discard"))
     ap.add_argument("--dir", default=None, help="file system for --sink disk (default $TMPDIR)")
     ap.add_argument("--warmup-frames", type=int, default=120)
+    ap.add_argument("--prep-workers", type=int, default=-1)
     a = ap.parse_args()
     from constructionsceneposeestimation_amd.generate import generate, parse_outputs
     outputs = parse_outputs(a.outputs)
@@ -73,7 +74,7 @@ def main():
         os.makedirs(out)
         t0 = time.perf_counter()
         s = generate(out, list(range(a.frames)), a.workload, seed=0, batch=a.batch, writers=a.writers,
-                     outputs=outputs, renderers=a.renderers, sink=a.sink)
+                     outputs=outputs, renderers=a.renderers, sink=a.sink, prep_workers=a.prep_workers)
         dt = time.perf_counter() - t0
         size = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(out) for f in fs)
         shutil.rmtree(out)
@@ -85,7 +86,7 @@ def main():
                "successful": s["counters"]["successful_frames"],
                "d2h_bytes_per_frame": tp["d2h_bytes_per_frame"], "d2h_gbs": tp["d2h_gbs"],
                "ids_wire_bytes": tp.get("ids_wire_bytes"),
-               "render_busy": tp["render_busy"], "renderers": tp["renderers"],
+               "prep_workers": tp.get("prep_workers"), "render_busy": tp["render_busy"], "renderers": tp["renderers"],
                "render_thread": tp["render_thread"], "main_thread": tp["main_thread"],
                "writers": tp["writers"], "writer_busy": tp["writer_busy"], "writer_task_s": tp["writer_task_s"],
                "bytes_on_disk_per_frame": round(size / a.frames) if a.sink == "disk" else None,
