@@ -198,7 +198,10 @@ def generate(out_dir: str, frames: List[int], workload: str = "C3", seed: int = 
     # encode and copy overlap the next ones' render (C3 1080p into RAM, 16
     # writers: 1,038 frames/s with two, 846 with one; at steady state with the
     # files to /dev/null, three: 1,823 / 515 frames/s without / with the point
-    # cloud, two: 1,739 / 505; profiles/r05/generate_steady.json).
+    # cloud, two: 1,739 / 505; profiles/r05/generate_steady.json.  Round 6, with
+    # the 1-byte id wire and two prep workers, batches of 60: three 2,028-2,150,
+    # four 2,029-2,041, three with batches of 120 1,912-1,975 frames/s without
+    # the point cloud; profiles/r06/ab/prep_workers/).
     n_rend = renderers or (3 if gpu_files else 1)
     # the writer processes start here, before this process touches the GPU
     pool = WriterPool(output_spec(batch, wl.height, wl.width, wl.n_keypoints(), scene_labels(wl.scene), want),
