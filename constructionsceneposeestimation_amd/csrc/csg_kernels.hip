@@ -574,7 +574,9 @@ __device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b
       ot &= v[k].y < 0.0f;
       ob &= v[k].y > Hf * v[k].w;
     }
-    if (!(on | of | ol | orr | ot | ob)) {
+    if ((DBG(b.dbg) & 0x10000u) && !(on | of | ol | orr | ot | ob)) {   // ablation: stop after the frustum test
+      if (v[0].x == 1.2345e-30f && b.inst) b.inst[0] = 1;              // (keeps the transform live)
+    } else if (!(on | of | ol | orr | ot | ob)) {
       const uint32_t uid = (i << s.uid_shift) | g;
       // Sutherland-Hodgman against W >= near over edges v0->v1, v1->v2, v2->v0
       // (each edge emits [start vertex if inside][intersection if crossing]),
