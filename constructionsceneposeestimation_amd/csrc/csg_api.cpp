@@ -86,8 +86,6 @@ struct csg_ctx {
   uint32_t n_inst = 0, n_meshes = 0, n_materials = 0;
   uint64_t n_tris_total = 0;
   DevBuf<float> tri_pos, tri_uv;       // de-indexed triangle soup (see SceneDev)
-  DevBuf<float> cvert;                 // each 256-triangle slice's distinct vertices (SceneDev::cvert)
-  DevBuf<uint32_t> ctri;               // each soup triangle's vertices in its slice (SceneDev::ctri)
   DevBuf<InstDesc> inst;
   std::vector<MatDesc> h_mats;
   std::vector<MatDesc> h_set_mats;      // [sets][n_materials] as uploaded
@@ -364,7 +362,7 @@ void csg_destroy(csg_ctx* c) {
   // (every batch's stream waits for its copies and id widening on the copy
   // stream, copy_done; synchronized here too before the buffers they read go)
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
-  c->tri_pos.release(); c->tri_uv.release(); c->cvert.release(); c->ctri.release(); c->inst.release(); c->set_mats.release(); c->iset.release(); c->lights.release();
+  c->tri_pos.release(); c->tri_uv.release(); c->inst.release(); c->set_mats.release(); c->iset.release(); c->lights.release();
   c->chunks.release();
   c->texels.release();
   c->aquad.release();
@@ -461,39 +459,6 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
       }
     }
   }
-  // Per mesh, per 256-triangle slice (a chunk's triangles): the slice's
-  // distinct vertices (object space) and each triangle's three as 10-bit
-  // indices into them, for k_setup's per-vertex transform (CSG_SETUP_VERTS).
-  std::vector<float> cvert;
-  std::vector<uint32_t> ctri(std::max<size_t>(n_soup, 1), 0u);
-  std::vector<std::vector<uint2>> slices(n_meshes);   // per mesh, per slice: (vbase, nverts)
-  {
-    std::vector<int32_t> local;
-    for (uint32_t m = 0; m < n_meshes; ++m) {
-      const MeshDesc& d = md[m];
-      local.assign(meshes[m].n_vertices, -1);
-      for (uint32_t s0 = 0; s0 < d.ntris; s0 += kBlock) {
-        const uint32_t vb = (uint32_t)(cvert.size() / 3), n = std::min<uint32_t>(kBlock, d.ntris - s0);
-        std::vector<uint32_t> used;
-        for (uint32_t t = s0; t < s0 + n; ++t) {
-          const size_t g = (size_t)d.tbase + t;
-          uint32_t pk = 0;
-          for (int k = 0; k < 3; ++k) {
-            const uint32_t vi = tris[g * 3 + k];
-            if (local[vi] < 0) {
-              local[vi] = (int32_t)used.size();
-              used.push_back(vi);
-              cvert.insert(cvert.end(), &pos[((size_t)d.vbase + vi) * 3], &pos[((size_t)d.vbase + vi) * 3] + 3);
-            }
-            pk |= (uint32_t)local[vi] << (10 * k);
-          }
-          ctri[g] = pk;
-        }
-        for (uint32_t vi : used) local[vi] = -1;
-        slices[m].push_back(make_uint2(vb, (uint32_t)used.size()));
-      }
-    }
-  }
   std::vector<InstDesc> idesc(n_inst);
   std::vector<Chunk> ch;
   std::vector<float> models((size_t)n_inst * 16);
@@ -511,8 +476,6 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
       c0.start = s0;
       c0.count = std::min<uint32_t>(kBlock, nt - s0);
       c0.soup = md_i.tbase + s0;   // soup index of the chunk's first triangle
-      c0.vbase = slices[inst[i].mesh][s0 / kBlock].x;
-      c0.nverts = slices[inst[i].mesh][s0 / kBlock].y;
       for (int a = 0; a < 3; ++a) { c0.lo[a] = INFINITY; c0.hi[a] = -INFINITY; }
       for (uint32_t t = s0; t < s0 + c0.count; ++t)
         for (int k = 0; k < 3; ++k) {
@@ -526,10 +489,6 @@ int csg_upload_scene(csg_ctx* c, const csg_mesh* meshes, uint32_t n_meshes, cons
   if (ch.empty()) return c->fail(CSG_ERR_INVALID, "upload_scene: no triangles");
   HIP_TRY(c, c->tri_pos.alloc(std::max<size_t>(tri_pos.size(), 9)));
   HIP_TRY(c, c->tri_uv.alloc(std::max<size_t>(tri_uv.size(), 6)));
-  HIP_TRY(c, c->cvert.alloc(std::max<size_t>(cvert.size(), 3)));
-  HIP_TRY(c, c->ctri.alloc(ctri.size()));
-  if (!cvert.empty()) HIP_TRY(c, hipMemcpy(c->cvert.p, cvert.data(), cvert.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->ctri.p, ctri.data(), ctri.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(c, c->inst.alloc(n_inst));
   HIP_TRY(c, c->chunks.alloc(ch.size()));
   HIP_TRY(c, hipMemcpy(c->tri_pos.p, tri_pos.data(), tri_pos.size() * 4, hipMemcpyHostToDevice));
@@ -893,7 +852,6 @@ static int ensure_work(csg_ctx* c) {
 static SceneDev scene_dev(const csg_ctx* c) {
   SceneDev s{};
   s.tri_pos = c->tri_pos.p; s.tri_uv = c->tri_uv.p; s.inst = c->inst.p;
-  s.cvert = c->cvert.p; s.ctri = c->ctri.p;
   s.texd = c->texd.p; s.texels = c->texels.p; s.aquad = c->aquad.p; s.acls = c->acls.p; s.n_inst = c->n_inst;
   s.W = c->cfg.width; s.H = c->cfg.height;
   s.tiles_x = c->tiles_x; s.tiles_y = c->tiles_y; s.n_tiles = c->n_tiles;

@@ -66,7 +66,7 @@ struct Chunk {                    // <= 256 triangles of one instance + their ob
   uint32_t inst, start, count;
   uint32_t soup;                  // soup index of triangle `start` (the mesh's base + start)
   float lo[3], hi[3];
-  uint32_t vbase, nverts;         // the chunk's distinct vertices in SceneDev::cvert (<= 3 x 256)
+  uint32_t pad2[2];
 };
 static_assert(sizeof(Chunk) == 48, "Chunk layout");
 
@@ -122,8 +122,6 @@ static_assert(sizeof(Slab) == 32, "Slab layout");
 struct SceneDev {
   const float* tri_pos;        // [T][3][3] object space
   const float* tri_uv;         // [T][3][2] (zeros for meshes without uvs)
-  const float* cvert;          // [V'][3] object space: each chunk slice's distinct vertices (Chunk::vbase)
-  const uint32_t* ctri;        // [T] a triangle's 3 vertices in its slice's cvert, 10 bits each
   const InstDesc* inst;        // [I]
   const TexDesc* texd;
   const uint8_t* texels;        // RGBA8, all textures back to back (TexDesc.offset in texels)

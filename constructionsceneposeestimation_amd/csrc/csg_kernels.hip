@@ -507,28 +507,17 @@ __device__ __forceinline__ CullOut corner_out(const SceneDev& s, const Chunk& ch
                  Y < -tol, Y > (float)s.H * Wc + tol * (float)s.H};
 }
 
-// CSG_SETUP_VERTS (A/B): the chunk's distinct vertices (SceneDev::cvert,
-// Chunk::vbase / nverts) are transformed once per block into LDS with their
-// reciprocal 1/W, and each triangle reads its three from there (SceneDev::
-// ctri) instead of transforming its three soup corners: the same dot products
-// and reciprocals per vertex, so the same bits.
-#ifndef CSG_SETUP_VERTS
-#define CSG_SETUP_VERTS 0
-#endif
-#if CSG_SETUP_VERTS
-constexpr uint32_t kChunkVerts = 3 * kBlock;   // distinct vertices of a chunk, at most
-#endif
-
 // The spec's per-vertex 1/W (spec 3): W >= near_clip > 2^-126 after near-plane
 // clipping, so below 2^126 the Newton reciprocal is the IEEE one (rcp_ieee);
 // the division only past that (never taken by real scenes: a uniform branch)
 __device__ __forceinline__ float rcp_w(float w) { return w <= 0x1p126f ? rcp_ieee(w) : 1.0f / w; }
 
 // The records of one chunk of triangles for frame f (one triangle per thread
-// of a 256-thread block; `sw` is the calling wave's record stage; `vtx` the
-// block's vertex table, CSG_SETUP_VERTS only).
+// of a 256-thread block; `sw` is the calling wave's record stage).  (A
+// per-vertex variant -- each slice's distinct vertices transformed once into
+// LDS -- was bit-exact and 8% slower: profiles/r06/ab/setup_verts.txt.)
 __device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b, const Chunk& ch, uint32_t f,
-                                            int tid, int lane, uint4* sw, float4* vtx);
+                                            int tid, int lane, uint4* sw);
 
 // Grid: x = frame (fast), (y, z) = chunk.  Consecutive workgroups take the
 // same chunk for successive frames, so a chunk's triangles (and its clip
@@ -552,32 +541,13 @@ __global__ __launch_bounds__(256) void k_setup(SceneDev s, BatchDev b, const Chu
   }
   static_assert(16 * kRecGroups <= 2 * 64, "two chunk stores per lane");
   __shared__ uint4 tstage[kBlock / 64][16 * kRecGroups];
-#if CSG_SETUP_VERTS
-  __shared__ float4 vtx[kChunkVerts];
-#else
-  float4* vtx = nullptr;
-#endif
-  setup_chunk(s, b, ch, f, tid, lane, tstage[tid >> 6], vtx);
+  setup_chunk(s, b, ch, f, tid, lane, tstage[tid >> 6]);
 }
 
 __device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b, const Chunk& ch, uint32_t f,
-                                            int tid, int lane, uint4* sw, float4* vtx) {
+                                            int tid, int lane, uint4* sw) {
   const uint32_t i = ch.inst;
   const float* Cm = b.clip + ((size_t)f * s.n_inst + i) * 12;
-#if CSG_SETUP_VERTS
-  {   // the chunk's vertices, once each: (X, Y, W, 1/W)
-    float c[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) c[k] = Cm[k];
-    for (uint32_t t = (uint32_t)tid; t < ch.nverts; t += kBlock) {
-      const float* p = s.cvert + (size_t)(ch.vbase + t) * 3;
-      const float px = p[0], py = p[1], pz = p[2];
-      const float W = dot4(c + 8, px, py, pz);
-      vtx[t] = make_float4(dot4(c + 0, px, py, pz), dot4(c + 4, px, py, pz), W, rcp_w(W));
-    }
-    __syncthreads();
-  }
-#endif
 
   // Records: groups 0-1 per sub-triangle (r0, r1: named, never runtime-
   // indexed, which would put them in scratch), groups 2-4 shared (the
@@ -588,20 +558,6 @@ __device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b
   if ((uint32_t)tid < ch.count) {
     const uint32_t g = ch.soup + tid;   // soup index (no instance-table load on the way)
     Cv3 v[3];
-#if CSG_SETUP_VERTS
-    float rv[3];
-    {
-      const uint32_t pk = s.ctri[g];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float4 q = vtx[(pk >> (10 * k)) & 1023u];
-        v[k].x = q.x;
-        v[k].y = q.y;
-        v[k].w = q.z;
-        rv[k] = q.w;
-      }
-    }
-#else
     float c[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) c[k] = Cm[k];
@@ -613,7 +569,6 @@ __device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b
       v[k].y = dot4(c + 4, px, py, pz);
       v[k].w = dot4(c + 8, px, py, pz);
     }
-#endif
     const float nearc = s.near_clip, farc = s.far_clip;
     const float Wf = (float)s.W, Hf = (float)s.H;
     bool on = true, of = true, ol = true, orr = true, ot = true, ob = true;
@@ -678,14 +633,8 @@ __device__ __forceinline__ void setup_chunk(const SceneDev& s, const BatchDev& b
       auto emit_tri = [&](const Cv3& a, const Cv3& bb, const Cv3& cc) {
         emit_tri_r(a, rcp_w(a.w), bb, rcp_w(bb.w), cc, rcp_w(cc.w));
       };
-#if CSG_SETUP_VERTS
-      if (in0 && in1 && in2) emit_tri_r(v[0], rv[0], v[1], rv[1], v[2], rv[2]);   // unclipped: the table's 1/W
-      else
-#endif
-      {
-        if (nq >= 3) emit_tri(q0, q1, q2);
-        if (nq >= 4) emit_tri(q0, q2, q3);
-      }
+      if (nq >= 3) emit_tri(q0, q1, q2);
+      if (nq >= 4) emit_tri(q0, q2, q3);
       // A record exists iff det != 0 and the screen test passes, in either
       // order: the homogeneous setup, its IEEE reciprocal and the material
       // loads are spent only on the few triangles that cover a pixel centre
